@@ -1,0 +1,131 @@
+/*
+ * vit_hip.h -- C ABI of libvit_hip.so, the MI355X (gfx950) kernels behind the
+ * ViT training step of seemadhungana/ViT-Project.
+ *
+ * The reference is pure Python: its hot path reaches GPU code only through
+ * torch ops called from timm's VisionTransformer (external) and from its own
+ * training loops.  Each entry point below replaces one of those ops; the
+ * reference call site it serves is cited as FILE:LINE with
+ *   VIT  = Training/vit_training/baseline/train_vit_sgd.py
+ *   MEAS = Training/vit_training/single_epoch/measure_single_epoch_perturbation_effect.py
+ *   NEWP = Training/functions/new_cvpr_train_behavior_things_pipeline.py
+ *
+ * Conventions: plain device pointers and sizes; `stream` is a hipStream_t;
+ * every function returns 0 or a hipError_t code and never allocates, frees or
+ * synchronises (graph-capture safe).  dtype codes: 0 = f32, 1 = bf16.
+ * Row strides (ld*) are in elements.
+ */
+#ifndef VIT_HIP_H
+#define VIT_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum { VIT_DTYPE_F32 = 0, VIT_DTYPE_BF16 = 1 };
+enum { VIT_LAYOUT_RC = 0, VIT_LAYOUT_CR = 1 };
+enum {
+  VIT_EPI_STORE = 0,      /* C = acc (+bias)                                   */
+  VIT_EPI_BIAS_GELU = 1,  /* C = pre = acc+bias, aux_out = gelu_erf(pre)       */
+  VIT_EPI_RESID = 2,      /* C (f32) = resid + acc + bias                      */
+  VIT_EPI_GELU_BWD = 3,   /* C = acc * gelu_erf'(pre)                          */
+  VIT_EPI_PATCH = 4,      /* patch-embed row remap + pos_embed                 */
+  VIT_EPI_BIAS_QGELU = 5, /* QuickGELU variant (OpenAI CLIP towers)            */
+  VIT_EPI_QGELU_BWD = 6
+};
+
+int vit_abi_version(void);
+
+/* Generic MFMA GEMM C[i][j] = epi(sum_r P(i,r) Q(j,r)); layouts RC (r contiguous)
+ * or CR (i/j contiguous).  Backs every nn.Linear of timm's ViT reached from
+ * VIT:139 (forward) and VIT:142 (backward). */
+int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int M, int N, int R,
+             const void* P, int64_t ldp, const void* Q, int64_t ldq, void* C, int64_t ldc,
+             const float* bias, const void* aux, int64_t ld_aux, void* aux_out, int allow_fast, void* stream);
+
+/* F.linear forward, Y = X W^T + b with fused epilogue (timm Attention.qkv/proj,
+ * Mlp.fc1+GELU / fc2 + residual, head; under VIT:138-139 autocast). */
+int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const void* X, int64_t ldx,
+                   const void* W, const float* bias, void* Y, int64_t ldy, const void* resid,
+                   void* act_out, void* stream);
+
+/* F.linear input gradient dX = dY W (+ GELU' epilogue) -- autograd of VIT:142. */
+int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, const void* dY, int64_t lddy,
+                     const void* W, void* dX, int64_t lddx, const void* pre, void* stream);
+
+/* F.linear weight gradient dW (f32) = dY^T X, split-K over rows with fp32 slabs
+ * in `workspace` (>= split*N*K*4 bytes) -- autograd of VIT:142. */
+int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t lddy, const void* X,
+                     int64_t ldx, float* dW, int split, void* workspace, int64_t ws_bytes, void* stream);
+
+/* Column sums (bias gradients): out[N] = sum_i X[i][:] -- autograd of VIT:142. */
+int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, float* partial,
+               int64_t partial_floats, int accumulate, void* stream);
+
+/* timm PatchEmbed Conv2d(3,768,16,16) as GEMM over unfolded patches, writing
+ * rows b*(np+1)+1+p of the f32 token stream with pos_embed added (VIT:139). */
+int vit_patch_embed_fwd(int dtype, int B, int np, int D, int K, const void* U, const void* W,
+                        const float* bias, const float* pos, float* x, void* stream);
+/* Conv2d 16/16 unfold: img f32 [B,C,H,W] -> U [B*np, C*ps*ps] (column = c*ps*ps+ky*ps+kx). */
+int vit_patch_unfold(int dtype, int B, int C, int Hi, int Wi, int ps, const float* img, void* U, void* stream);
+/* cat(cls_token) + pos_embed[0] into row 0 of every image (timm _pos_embed). */
+int vit_cls_pos_fill(int B, int S, int D, float* x, const float* cls, const float* pos, void* stream);
+/* d pos_embed [S,D] = sum_b dx[b]; d cls_token = d pos_embed[0]. */
+int vit_pos_grad(int B, int S, int D, const float* dx, float* dpos, float* dcls, void* stream);
+
+/* F.layer_norm forward (timm norm1/norm2/norm, eps 1e-6), one wave per row; saves mean/rstd. */
+int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x, int64_t ldx, void* y,
+                       int64_t ldy, const float* w, const float* b, float* mean, float* rstd, float eps,
+                       void* stream);
+/* LayerNorm backward with fused residual-gradient add, optional GEMM-dtype copy
+ * of dx (optionally dropping CLS rows), dgamma/dbeta. */
+int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x, int64_t ldx,
+                       const void* dy, int64_t lddy, const float* w, const float* mean, const float* rstd,
+                       const float* dres, int64_t ldres, float* dx, int64_t lddx, void* dx_copy, int64_t ld_copy,
+                       int dtype_copy, int compact_np, float* dgamma, float* dbeta, float* partial,
+                       int64_t partial_floats, void* stream);
+
+/* F.scaled_dot_product_attention(q,k,v) (timm Attention, no mask, head_dim 64,
+ * N <= 288) reading q/k/v in place from the qkv GEMM output; lse [B*H*N] f32. */
+int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, void* o,
+                 int64_t ld_o, float* lse, float scale, void* stream);
+/* SDPA backward into dqkv (qkv layout). delta_ws >= B*H*N floats (f32 path). */
+int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, const void* o,
+                 int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
+                 float* delta_ws, float scale, void* stream);
+
+/* torch.nn.functional.cross_entropy(outputs, targets) mean (VIT:140) and its gradient. */
+int vit_cross_entropy_fwd(int B, int C, const float* logits, int64_t ld, const int64_t* target, float* row_lse,
+                          float* row_loss, float* loss, void* stream);
+int vit_cross_entropy_bwd(int dtype_out, int B, int C, const float* logits, int64_t ld, const int64_t* target,
+                          const float* row_lse, const float* grad_loss, void* dlogits, int64_t ldd, void* stream);
+
+/* torch.optim.SGD(lr, momentum, weight_decay).step() over all parameters in one
+ * launch (VIT:143-144, VIT:294-299).  tensors: {float* p; const float* g; float* buf;
+ * bf16* shadow; int64 n}[], chunks: {int tensor; int pad; int64 start}[] (4096 elems). */
+int vit_sgd_step(const void* tensors, const void* chunks, int nchunks, const float* lr, float momentum,
+                 float weight_decay, void* stream);
+int vit_sgd_chunk_size(void);
+int vit_sgd_tensor_bytes(void);
+int vit_sgd_chunk_bytes(void);
+
+/* DoRALayer.weight (NEWP:447-463): W[out,in] = (m * (D + (B@A)s) / (||.||_col + 1e-8))^T,
+ * and its backward (dm, dA, dB) for AdamW (NEWP:1000-1001). */
+int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, const float* B, const float* D,
+                        float scaling, float* W, float* nu, float* DnT_ws, float* colsq_ws, void* stream);
+int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, const float* B, const float* gW,
+                        const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
+                        float* sdDnT_ws, void* unused, void* stream);
+/* torch.optim.AdamW step (NEWP:1181): tensors {p, g, exp_avg, exp_avg_sq, n}[]. */
+int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, const float* lr, const float* step,
+                   float beta1, float beta2, float eps, float weight_decay, void* stream);
+
+/* helpers */
+int vit_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
+int vit_zero(void* p, int64_t bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VIT_HIP_H */

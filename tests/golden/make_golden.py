@@ -1,0 +1,237 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+Run in the build container (NOT on the GPU box -- /root/reference does not exist there):
+
+    python tests/golden/make_golden.py
+
+What it pins:
+  1. The oracle's ViT restatement (oracle/vit_ref.py) against ``transformers``
+     ViTForImageClassification on identical weights (timm is absent; transformers
+     is an independent implementation of the same architecture).  Fixtures:
+     vit_tiny_golden.pt (full grads) and vit_b16_golden.pt (bs=2 logits, CLS
+     features, per-parameter grad norms + slices).
+  2. The reference's own Python, imported from /root/reference with stub modules
+     for the absent third-party packages (torchvision, timm, the CLIP-HBA fork):
+       - DoRALayer.weight + autograd grads  (NEWP:407-463)    -> dora_golden.pt
+       - behavioral_RSA                      (NEWP:605-654)    -> rsa_golden.npz
+       - CosineAnnealingLRWithWarmup         (VIT:206-244)     -> lr_golden.json
+     The reference source itself is never copied; only input/output vectors are.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import tempfile
+import types
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from oracle import vit_ref as R  # noqa: E402
+
+REF = "/root/reference"
+
+
+def _stub_reference_imports():
+    for name in ["torchvision", "torchvision.transforms", "torchvision.datasets", "timm", "src",
+                 "src.models", "src.models.CLIPs", "src.models.CLIPs.clip_hba",
+                 "src.models.clip_hba_utils"]:
+        sys.modules.setdefault(name, types.ModuleType(name))
+    sys.modules["torchvision"].transforms = sys.modules["torchvision.transforms"]
+    sys.modules["torchvision"].datasets = sys.modules["torchvision.datasets"]
+    sys.modules["src.models.CLIPs.clip_hba"].clip = types.SimpleNamespace()
+    sys.path.insert(0, os.path.join(REF, "Training"))
+    sys.path.insert(0, os.path.join(REF, "Training", "vit_training", "baseline"))
+
+
+# ----------------------------------------------------------------------------
+# 1. ViT restatement vs transformers
+# ----------------------------------------------------------------------------
+
+def to_hf(p, cfg):
+    from transformers import ViTConfig as HFC, ViTForImageClassification
+    hc = HFC(hidden_size=cfg.embed_dim, num_hidden_layers=cfg.depth, num_attention_heads=cfg.num_heads,
+             intermediate_size=cfg.mlp_dim, hidden_act="gelu", layer_norm_eps=cfg.eps,
+             image_size=cfg.img_size, patch_size=cfg.patch_size, num_channels=cfg.in_chans,
+             num_labels=cfg.num_classes, qkv_bias=True, hidden_dropout_prob=0.0,
+             attention_probs_dropout_prob=0.0)
+    m = ViTForImageClassification(hc).eval()
+    D = cfg.embed_dim
+    sd = OrderedDict()
+    sd["vit.embeddings.cls_token"] = p["cls_token"]
+    sd["vit.embeddings.position_embeddings"] = p["pos_embed"]
+    sd["vit.embeddings.patch_embeddings.projection.weight"] = p["patch_embed.proj.weight"]
+    sd["vit.embeddings.patch_embeddings.projection.bias"] = p["patch_embed.proj.bias"]
+    for i in range(cfg.depth):
+        b, h = f"blocks.{i}.", f"vit.layers.{i}."   # transformers 5.x key layout
+        w, bb = p[b + "attn.qkv.weight"], p[b + "attn.qkv.bias"]
+        for j, n in enumerate(["q_proj", "k_proj", "v_proj"]):
+            sd[h + f"attention.{n}.weight"] = w[j * D:(j + 1) * D]
+            sd[h + f"attention.{n}.bias"] = bb[j * D:(j + 1) * D]
+        sd[h + "attention.o_proj.weight"] = p[b + "attn.proj.weight"]
+        sd[h + "attention.o_proj.bias"] = p[b + "attn.proj.bias"]
+        sd[h + "layernorm_before.weight"] = p[b + "norm1.weight"]
+        sd[h + "layernorm_before.bias"] = p[b + "norm1.bias"]
+        sd[h + "layernorm_after.weight"] = p[b + "norm2.weight"]
+        sd[h + "layernorm_after.bias"] = p[b + "norm2.bias"]
+        sd[h + "mlp.fc1.weight"] = p[b + "mlp.fc1.weight"]
+        sd[h + "mlp.fc1.bias"] = p[b + "mlp.fc1.bias"]
+        sd[h + "mlp.fc2.weight"] = p[b + "mlp.fc2.weight"]
+        sd[h + "mlp.fc2.bias"] = p[b + "mlp.fc2.bias"]
+    sd["vit.layernorm.weight"] = p["norm.weight"]
+    sd["vit.layernorm.bias"] = p["norm.bias"]
+    sd["classifier.weight"] = p["head.weight"]
+    sd["classifier.bias"] = p["head.bias"]
+    missing, unexpected = m.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all("pooler" in k for k in missing), missing
+    return m
+
+
+def vit_fixture(cfg, B, seed, full_grads):
+    torch.manual_seed(seed)
+    p = R.init_params(cfg, seed=seed, random_affine=True)
+    g = torch.Generator().manual_seed(seed + 1)
+    x = torch.randn(B, cfg.in_chans, cfg.img_size, cfg.img_size, generator=g)
+    y = torch.randint(0, cfg.num_classes, (B,), generator=g)
+    with torch.no_grad():
+        logits = R.forward(p, x, cfg)
+        feats = R.forward_features(p, x, cfg)
+        hf = to_hf(p, cfg)
+        hf_logits = hf(pixel_values=x).logits
+        hf_feats = hf.vit(pixel_values=x).last_hidden_state
+    rel = (logits - hf_logits).abs().max() / hf_logits.abs().max()
+    relf = (feats - hf_feats).abs().max() / hf_feats.abs().max()
+    print(f"  oracle vs transformers: logits rel {rel:.3e}, features rel {relf:.3e}")
+    assert rel < 1e-5 and relf < 1e-5
+    bufs = {}
+    pc = OrderedDict((k, v.clone()) for k, v in p.items())
+    loss, grads = R.train_step(pc, bufs, x, y, lr=0.1, cfg=cfg)
+    # grads against transformers autograd too
+    hf.zero_grad()
+    hl = torch.nn.functional.cross_entropy(hf(pixel_values=x).logits, y)
+    hl.backward()
+    gq = hf.vit.layers[0].attention.q_proj.weight.grad
+    D = cfg.embed_dim
+    relg = (grads["blocks.0.attn.qkv.weight"][:D] - gq).abs().max() / gq.abs().max()
+    print(f"  oracle vs transformers: loss {loss:.6f} vs {float(hl):.6f}, blk0 q-grad rel {relg:.3e}")
+    assert relg < 1e-4
+    fx = {"seed": seed, "B": B, "cfg": cfg.__dict__, "x_sum": float(x.sum()), "y": y,
+          "param_checksum": {k: float(v.double().sum()) for k, v in p.items()},
+          "logits": logits, "hf_logits": hf_logits, "cls_features": feats[:, 0].clone(),
+          "loss": loss, "hf_loss": float(hl),
+          "grad_norm": {k: float(v.norm()) for k, v in grads.items()},
+          "grad_slice": {k: v.flatten()[:64].clone() for k, v in grads.items()},
+          "param_after_slice": {k: v.flatten()[:64].clone() for k, v in pc.items()}}
+    if full_grads:
+        fx["grads"] = grads
+        fx["features"] = feats
+        fx["params_after"] = pc
+    return fx
+
+
+# ----------------------------------------------------------------------------
+# 2. reference functions imported from /root/reference
+# ----------------------------------------------------------------------------
+
+def dora_fixture():
+    _stub_reference_imports()
+    import functions.new_cvpr_train_behavior_things_pipeline as NEWP
+    out = {}
+    for (fin, fout, r) in [(96, 80, 8), (1024, 1024, 32), (768, 768, 32)]:
+        torch.manual_seed(1234 + fin)
+        base = torch.nn.Linear(fin, fout)
+        layer = NEWP.DoRALayer(base, r=r, dora_alpha=16, dora_dropout=0.1)
+        W = layer.weight
+        gW = torch.randn_like(W)
+        (W * gW).sum().backward()
+        rec = {"in": fin, "out": fout, "r": r, "scaling": layer.scaling,
+               "m": layer.m.detach().clone(), "A": layer.delta_D_A.detach().clone(),
+               "B": layer.delta_D_B.detach().clone(), "D": layer.D.clone(), "gW": gW,
+               "W": W.detach().clone(), "dm": layer.m.grad.clone(),
+               "dA": layer.delta_D_A.grad.clone(), "dB": layer.delta_D_B.grad.clone(),
+               "bias": layer.bias.detach().clone()}
+        if fin > 100:  # keep the committed file small: inputs are regenerated from the seed
+            rec = {k: v for k, v in rec.items() if k in ("in", "out", "r", "scaling")}
+            rec.update({"seed": 1234 + fin, "W_sum": float(W.double().sum()),
+                        "W_abs": float(W.double().abs().sum()), "W_row0": W[0, :64].detach().clone(),
+                        "dm": layer.m.grad.clone(), "dA_norm": float(layer.delta_D_A.grad.norm()),
+                        "dB_norm": float(layer.delta_D_B.grad.norm()),
+                        "dA_slice": layer.delta_D_A.grad[0, :64].clone(),
+                        "dB_slice": layer.delta_D_B.grad[0, :32].clone()})
+        out[f"{fin}x{fout}r{r}"] = rec
+    # trainable-parameter count of the CLIP-HBA DoRA setup (log: 183040)
+    out["clip_trainable"] = 2 * (1024 + 32 * 1024 + 1024 * 32) + (768 + 32 * 768 + 768 * 32)
+    return out
+
+
+def rsa_fixture():
+    _stub_reference_imports()
+    import scipy.io
+    import functions.new_cvpr_train_behavior_things_pipeline as NEWP
+    rng = np.random.default_rng(7)
+    res = {}
+    with tempfile.TemporaryDirectory() as td:
+        for name, dim in [("clip66", 66), ("vit768", 768)]:
+            emb = rng.standard_normal((48, dim)).astype(np.float32)
+            ref = rng.integers(0, 12, size=(48, 48)).astype(np.float64) / 11.0  # ties on purpose
+            ref = (ref + ref.T) / 2
+            np.fill_diagonal(ref, 0)
+            mat = os.path.join(td, f"{name}.mat")
+            scipy.io.savemat(mat, {"RDM48_triplet": ref})
+
+            class DS(torch.utils.data.Dataset):
+                RDM48_triplet_dir = mat
+
+                def __len__(self):
+                    return 48
+
+                def __getitem__(self, i):
+                    return f"img{i:02d}", torch.from_numpy(emb[i])
+
+            loader = torch.utils.data.DataLoader(DS(), batch_size=8, shuffle=False)
+            rho, p, rdm = NEWP.behavioral_RSA(torch.nn.Identity(), loader, "cpu", logger=None)
+            res[f"{name}_emb"] = emb
+            res[f"{name}_ref"] = ref
+            res[f"{name}_rho"] = np.float64(rho)
+            res[f"{name}_p"] = np.float64(p)
+            res[f"{name}_rdm"] = rdm
+    return res
+
+
+def lr_fixture():
+    _stub_reference_imports()
+    import train_vit_sgd as VIT
+    net = torch.nn.Linear(2, 2)
+    opt = torch.optim.SGD(net.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+    sch = VIT.CosineAnnealingLRWithWarmup(opt, warmup_epochs=5, max_epochs=100, eta_min=0)
+    lrs = []
+    for _ in range(100):
+        lrs.append(opt.param_groups[0]["lr"])  # LR used while training this epoch
+        sch.step()
+    return {"base_lr": 0.1, "warmup_epochs": 5, "max_epochs": 100, "lr_per_epoch": lrs}
+
+
+def main():
+    torch.set_num_threads(os.cpu_count() or 8)
+    print("ViT tiny fixture")
+    torch.save(vit_fixture(R.VIT_TINY, B=3, seed=11, full_grads=True), os.path.join(HERE, "vit_tiny_golden.pt"))
+    print("ViT-B/16 fixture (bs=2)")
+    torch.save(vit_fixture(R.VIT_B16, B=2, seed=0, full_grads=False), os.path.join(HERE, "vit_b16_golden.pt"))
+    print("DoRA fixture (reference DoRALayer)")
+    torch.save(dora_fixture(), os.path.join(HERE, "dora_golden.pt"))
+    print("RSA fixture (reference behavioral_RSA)")
+    np.savez(os.path.join(HERE, "rsa_golden.npz"), **rsa_fixture())
+    print("LR fixture (reference CosineAnnealingLRWithWarmup)")
+    with open(os.path.join(HERE, "lr_golden.json"), "w") as f:
+        json.dump(lr_fixture(), f, indent=1)
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

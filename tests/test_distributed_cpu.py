@@ -1,0 +1,70 @@
+"""CPU (gloo, world_size 2): the data-parallel gradient averaging and the sweep sharder."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from vit_amd import parallel
+    r, w, _ = parallel.init_from_env(backend="gloo")
+    assert (r, w) == (rank, world)
+    g = torch.Generator().manual_seed(rank)
+    flat = torch.randn(1_000_003, generator=g)
+    expect = sum(torch.randn(1_000_003, generator=torch.Generator().manual_seed(k)) for k in range(world)) / world
+    parallel.allreduce_flat(flat, bucket_mb=1.0)
+    q.put((rank, float((flat - expect).abs().max())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_allreduce_flat_world2():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err in res:
+        assert err < 1e-5, (rank, err)
+
+
+def test_shard_conditions_partition_and_chains():
+    from vit_amd import parallel
+    conds = parallel.length_sweep_conditions()
+    assert len(conds) == 128
+    world = 8
+    shards = [parallel.shard_conditions(conds, world, r) for r in range(world)]
+    allc = sorted(c for s in shards for c in s)
+    assert allc == sorted(conds)                       # exact partition
+    for s in shards:                                   # start-epoch chains stay together
+        starts = {c[0] for c in s}
+        for st in starts:
+            assert sorted(c for c in conds if c[0] == st) == sorted(c for c in s if c[0] == st)
+    loads = [sum(c[1] for c in s) for s in shards]
+    assert max(loads) - min(loads) <= max(c[1] for c in conds) * 2
+    assert shards == [parallel.shard_conditions(conds, world, r) for r in range(world)]  # deterministic
+
+
+def test_bucket_bounds():
+    from vit_amd import parallel
+    assert parallel.bucket_bounds(10, 4) == [(0, 4), (4, 8), (8, 10)]
+    assert parallel.bucket_bounds(86_567_656, 16 * 1024 * 1024)[-1][1] == 86_567_656

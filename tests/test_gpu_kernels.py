@@ -1,0 +1,332 @@
+"""GPU: every HIP kernel against a CPU fp32 reference of the same op.
+
+Tolerances: f32-in/f32-out kernels 1e-5 relative to the output scale; bf16
+inputs are rounded to bf16 before the CPU reference so only accumulation order
+and the output rounding differ (bf16 out: 1e-2 of scale; f32 out: 1e-5).
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from vit_amd import _lib as L  # noqa: E402
+from vit_amd import ops  # noqa: E402
+
+DEV = "cuda"
+
+
+def _close(got, ref, rel, what=""):
+    got = got.detach().float().cpu()
+    ref = ref.detach().float().cpu()
+    scale = ref.abs().max().item() + 1e-12
+    err = (got - ref).abs().max().item()
+    assert err <= rel * scale, f"{what}: max err {err:.3e} > {rel:.1e} * scale {scale:.3e}"
+
+
+def _rnd(*shape, dtype=torch.float32, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dtype)
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _lib_loaded():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    L.load()
+
+
+# ---------------------------------------------------------------------------- GEMM
+
+@pytest.mark.parametrize("M,N,K", [(256, 384, 192), (1024, 768, 768), (384, 256, 3072)])
+@pytest.mark.parametrize("out_dtype", [torch.float32, torch.bfloat16])
+def test_linear_fwd_fast_bf16(M, N, K, out_dtype):
+    x = _rnd(M, K, seed=1, dtype=torch.bfloat16)
+    w = _rnd(N, K, seed=2, scale=0.05, dtype=torch.bfloat16)
+    b = _rnd(N, seed=3)
+    ref = x.float() @ w.float().T + b
+    y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), out_dtype=out_dtype)
+    _close(y, ref, 1e-5 if out_dtype == torch.float32 else 8e-3, "fwd")
+
+
+def test_linear_fwd_asymmetric_identity():
+    # A = I with an asymmetric B catches a transposed C write (guide §3)
+    n = 256
+    x = torch.eye(n, dtype=torch.bfloat16)
+    w = (torch.arange(n * n, dtype=torch.float32).reshape(n, n) % 97).to(torch.bfloat16)
+    y = ops.linear_fwd(x.to(DEV), w.to(DEV), None, out_dtype=torch.float32)
+    assert torch.equal(y.cpu(), w.float().T.contiguous())
+
+
+def test_linear_epilogues_bf16():
+    M, N, K = 512, 384, 256
+    x = _rnd(M, K, seed=4, dtype=torch.bfloat16)
+    w = _rnd(N, K, seed=5, scale=0.06, dtype=torch.bfloat16)
+    b = _rnd(N, seed=6, scale=0.1)
+    acc = x.float() @ w.float().T + b
+    pre, act = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_BIAS_GELU)
+    _close(pre, acc, 8e-3, "pre")
+    _close(act, torch.nn.functional.gelu(pre.float().cpu()), 8e-3, "gelu")
+    resid = _rnd(M, N, seed=7)
+    out = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_RESID, resid=resid.to(DEV))
+    _close(out, resid + acc, 1e-5, "resid")
+    # in-place residual (out aliases resid)
+    r2 = resid.to(DEV)
+    ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_RESID, resid=r2, out=r2)
+    _close(r2, resid + acc, 1e-5, "resid inplace")
+    # quick gelu
+    pre_q, act_q = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_BIAS_QGELU)
+    p = pre_q.float().cpu()
+    _close(act_q, p * torch.sigmoid(1.702 * p), 8e-3, "qgelu")
+
+
+def test_linear_dgrad_and_gelu_bwd():
+    M, N, K = 512, 256, 384
+    dy = _rnd(M, N, seed=8, dtype=torch.bfloat16)
+    w = _rnd(N, K, seed=9, scale=0.05, dtype=torch.bfloat16)
+    ref = dy.float() @ w.float()
+    dx = ops.linear_dgrad(dy.to(DEV), w.to(DEV), out_dtype=torch.float32)
+    _close(dx, ref, 1e-5, "dgrad")
+    pre = _rnd(M, K, seed=10, dtype=torch.bfloat16)
+    pf = pre.float().requires_grad_(True)
+    torch.nn.functional.gelu(pf).backward(ref)
+    d = ops.linear_dgrad(dy.to(DEV), w.to(DEV), out_dtype=torch.bfloat16, epi=L.EPI_GELU_BWD, pre=pre.to(DEV))
+    _close(d, pf.grad, 8e-3, "gelu bwd")
+
+
+@pytest.mark.parametrize("M,N,K,split", [(1024, 256, 384, 1), (4096, 384, 256, 4), (6336, 256, 128, 7), (6304, 256, 128, 3)])
+def test_linear_wgrad(M, N, K, split):
+    dy = _rnd(M, N, seed=11, dtype=torch.bfloat16)
+    x = _rnd(M, K, seed=12, dtype=torch.bfloat16)
+    ref = dy.float().T @ x.float()
+    dw = ops.linear_wgrad(dy.to(DEV), x.to(DEV), split=split)
+    _close(dw, ref, 2e-5, "wgrad")
+
+
+def test_gemm_cr_rc_layout_fast():
+    # the fourth layout combination (P CR, Q RC) through the raw dispatcher
+    M, N, R = 256, 128, 192
+    P = _rnd(R, M, seed=13, dtype=torch.bfloat16)   # P(i,r) = P[r][i]
+    Q = _rnd(N, R, seed=14, dtype=torch.bfloat16)   # Q(j,r) = Q[j][r]
+    C = torch.empty(M, N, dtype=torch.float32, device=DEV)
+    Pd, Qd = P.to(DEV), Q.to(DEV)
+    L.call("vit_gemm", L.BF16, L.F32, L.LAY_CR, L.LAY_RC, L.EPI_STORE, M, N, R, Pd.data_ptr(), M, Qd.data_ptr(), R,
+           C.data_ptr(), N, None, None, 0, None, 1, L.stream_ptr())
+    _close(C, P.float().T @ Q.float().T, 1e-5, "cr-rc")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_generic_gemm_odd_shapes(dtype):
+    M, N, K = 37, 1000, 70
+    x = _rnd(M, K, seed=15, dtype=dtype)
+    w = _rnd(N, K, seed=16, scale=0.1, dtype=dtype)
+    b = _rnd(N, seed=17)
+    y = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), out_dtype=torch.float32)
+    _close(y, x.float() @ w.float().T + b, 1e-5, "generic fwd")
+    dy = _rnd(M, N, seed=18, dtype=dtype)
+    _close(ops.linear_dgrad(dy.to(DEV), w.to(DEV)), dy.float() @ w.float(), 1e-5, "generic dgrad")
+    _close(ops.linear_wgrad(dy.to(DEV), x.to(DEV)), dy.float().T @ x.float(), 1e-5, "generic wgrad")
+    _close(ops.linear_wgrad(dy.to(DEV), x.to(DEV), split=3), dy.float().T @ x.float(), 1e-5, "generic wgrad split")
+
+
+def test_colsum():
+    for dtype in (torch.float32, torch.bfloat16):
+        x = _rnd(3001, 768, seed=19, dtype=dtype)
+        _close(ops.colsum(x.to(DEV)), x.float().sum(0), 1e-5, "colsum")
+
+
+# ---------------------------------------------------------------------------- patch embed
+
+def test_patch_embed_fwd_and_unfold():
+    B, D = 3, 256
+    img = _rnd(B, 3, 64, 48, seed=20)
+    w = _rnd(D, 3, 16, 16, seed=21, scale=0.02)
+    b = _rnd(D, seed=22)
+    np_ = (64 // 16) * (48 // 16)
+    pos = _rnd(1, np_ + 1, D, seed=23)
+    cls = _rnd(1, 1, D, seed=24)
+    for dt, rel in ((torch.float32, 1e-5), (torch.bfloat16, 1e-2)):
+        U = ops.patch_unfold(img.to(DEV), 16, dt)
+        ref_u = img.unfold(2, 16, 16).unfold(3, 16, 16).permute(0, 2, 3, 1, 4, 5).reshape(B * np_, -1)
+        assert torch.equal(U.cpu(), ref_u.to(dt))
+        x = ops.patch_embed_fwd(U, w.reshape(D, -1).to(dt).to(DEV), b.to(DEV), pos.reshape(-1, D).to(DEV),
+                                cls.reshape(-1).to(DEV), B, np_)
+        y = torch.nn.functional.conv2d(img, w.to(dt).float(), b, stride=16).flatten(2).transpose(1, 2)
+        ref = torch.cat([cls.expand(B, -1, -1), y], 1) + pos
+        _close(x, ref, rel if dt == torch.float32 else 2e-3, f"patch {dt}")
+
+
+# ---------------------------------------------------------------------------- LayerNorm
+
+@pytest.mark.parametrize("D", [768, 1024, 64, 200])
+@pytest.mark.parametrize("xdt", [torch.float32, torch.bfloat16])
+def test_layer_norm_fwd_bwd(D, xdt):
+    M = 333
+    x = _rnd(M, D, seed=25, scale=2.0).to(xdt)
+    w = 1 + _rnd(D, seed=26, scale=0.2)
+    b = _rnd(D, seed=27, scale=0.1)
+    dy = _rnd(M, D, seed=28)
+    dres = _rnd(M, D, seed=29)
+    xr = x.float().requires_grad_(True)
+    wr, br = w.clone().requires_grad_(True), b.clone().requires_grad_(True)
+    yr = torch.nn.functional.layer_norm(xr, (D,), wr, br, 1e-6)
+    yr.backward(dy)
+    for ydt in (torch.float32, torch.bfloat16):
+        y, mean, rstd = ops.layer_norm_fwd(x.to(DEV), w.to(DEV), b.to(DEV), 1e-6, ydt)
+        _close(y, yr, 1e-5 if ydt == torch.float32 else 8e-3, "ln fwd")
+    y, mean, rstd = ops.layer_norm_fwd(x.to(DEV), w.to(DEV), b.to(DEV), 1e-6, torch.float32)
+    dx = torch.empty(M, D, device=DEV)
+    copy = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    dg = torch.empty(D, device=DEV)
+    db = torch.empty(D, device=DEV)
+    ops.layer_norm_bwd(x.to(DEV), D, dy.to(DEV), w.to(DEV), mean, rstd, dx, D, M, dres=dres.to(DEV), ldres=D,
+                       dx_copy=copy, ld_copy=D, dgamma=dg, dbeta=db)
+    _close(dx, xr.grad + dres, 1e-5, "ln dx")
+    _close(copy, xr.grad + dres, 8e-3, "ln dx copy")
+    _close(dg, wr.grad, 1e-5, "dgamma")
+    _close(db, br.grad, 1e-5, "dbeta")
+
+
+def test_layer_norm_bwd_compact_rows():
+    B, S, D = 3, 5, 768
+    x = _rnd(B * S, D, seed=30)
+    w, b = 1 + _rnd(D, seed=31, scale=0.1), _rnd(D, seed=32, scale=0.1)
+    dy = _rnd(B * S, D, seed=33)
+    y, mean, rstd = ops.layer_norm_fwd(x.to(DEV), w.to(DEV), b.to(DEV), 1e-6, torch.float32)
+    dx = torch.empty(B * S, D, device=DEV)
+    copy = torch.full((B * (S - 1), D), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.layer_norm_bwd(x.to(DEV), D, dy.to(DEV), w.to(DEV), mean, rstd, dx, D, B * S, dx_copy=copy, ld_copy=D,
+                       compact_np=S - 1)
+    want = dx.cpu().reshape(B, S, D)[:, 1:].reshape(-1, D)
+    _close(copy, want, 8e-3, "compact")
+
+
+# ---------------------------------------------------------------------------- attention
+
+def _sdpa_ref(qkv, B, H, N):
+    D = H * 64
+    q, k, v = qkv.float().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    q, k, v = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    s = (q @ k.transpose(-2, -1)) * 0.125
+    lse = torch.logsumexp(s, -1)
+    o = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * N, D)
+    return o, lse.reshape(-1), (q, k, v)
+
+
+@pytest.mark.parametrize("N", [197, 50, 257, 16])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_sdpa_fwd_bwd(N, dtype):
+    B, H = 2, 3
+    D = H * 64
+    qkv = _rnd(B * N, 3 * D, seed=34, scale=1.5).to(dtype)
+    do = _rnd(B * N, D, seed=35).to(dtype)
+    o_ref, lse_ref, (q, k, v) = _sdpa_ref(qkv, B, H, N)
+    o_ref.backward(do.float())
+    dq = q.grad.transpose(1, 2).reshape(B * N, D)
+    dk = k.grad.transpose(1, 2).reshape(B * N, D)
+    dv = v.grad.transpose(1, 2).reshape(B * N, D)
+    o, lse = ops.sdpa_fwd(qkv.to(DEV), B, H, N)
+    rel = 1e-5 if dtype == torch.float32 else 1.5e-2
+    _close(o, o_ref, rel, "o")
+    _close(lse, lse_ref, 1e-5 if dtype == torch.float32 else 2e-3, "lse")
+    # backward from the reference forward's o so only the bwd kernel is tested
+    dqkv = ops.sdpa_bwd(qkv.to(DEV), o_ref.detach().to(dtype).to(DEV), do.to(DEV), lse_ref.to(DEV), B, H, N)
+    g = dqkv.float().cpu()
+    rel = 1e-4 if dtype == torch.float32 else 3e-2
+    _close(g[:, :D], dq, rel, "dq")
+    _close(g[:, D:2 * D], dk, rel, "dk")
+    _close(g[:, 2 * D:], dv, rel, "dv")
+
+
+# ---------------------------------------------------------------------------- CE / SGD / misc
+
+def test_cross_entropy():
+    B, C = 37, 1000
+    logits = _rnd(B, C, seed=36, scale=3.0)
+    tgt = torch.randint(0, C, (B,), generator=torch.Generator().manual_seed(37))
+    lr_ = logits.clone().requires_grad_(True)
+    loss_ref = torch.nn.functional.cross_entropy(lr_, tgt)
+    loss_ref.backward(torch.tensor(0.5))
+    loss, row_lse = ops.cross_entropy_fwd(logits.to(DEV), tgt.to(DEV))
+    assert abs(loss.item() - loss_ref.item()) < 1e-5 * abs(loss_ref.item())
+    d = ops.cross_entropy_bwd(logits.to(DEV), tgt.to(DEV), row_lse, torch.tensor(0.5, device=DEV))
+    _close(d, lr_.grad, 1e-5, "dlogits")
+
+
+def test_fused_sgd_matches_torch_sgd_and_writes_shadow():
+    from vit_amd.optim import FusedSGD
+    torch.manual_seed(0)
+    shapes = [(768, 768), (1000,), (3, 5), (4097,)]
+    ps = [torch.nn.Parameter(torch.randn(s)) for s in shapes]
+    qs = [torch.nn.Parameter(p.detach().clone().to(DEV)) for p in ps]
+    for q in qs[:2]:
+        q._vit_shadow = torch.empty(q.shape, dtype=torch.bfloat16, device=DEV)
+    ref = torch.optim.SGD(ps, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    opt = FusedSGD(qs, lr=0.1, momentum=0.9, weight_decay=1e-4)
+    for step in range(3):
+        for p, q in zip(ps, qs):
+            g = torch.randn(p.shape)
+            p.grad = g.clone()
+            q.grad = g.to(DEV)
+        ref.step()
+        opt.step()
+        for p, q in zip(ps, qs):
+            _close(q, p, 1e-6, "sgd")
+    for q in qs[:2]:
+        assert torch.equal(q._vit_shadow.cpu(), q.detach().cpu().to(torch.bfloat16))
+
+
+def test_fused_adamw_matches_torch():
+    from vit_amd.optim import FusedAdamW
+    torch.manual_seed(1)
+    ps = [torch.nn.Parameter(torch.randn(s)) for s in [(32, 1024), (1024,), (7,)]]
+    qs = [torch.nn.Parameter(p.detach().clone().to(DEV)) for p in ps]
+    ref = torch.optim.AdamW(ps, lr=3e-4, weight_decay=0.01)
+    opt = FusedAdamW(qs, lr=3e-4, weight_decay=0.01)
+    for step in range(4):
+        for p, q in zip(ps, qs):
+            g = torch.randn(p.shape)
+            p.grad = g.clone()
+            q.grad = g.to(DEV)
+        ref.step()
+        opt.step()
+    for p, q in zip(ps, qs):
+        _close(q, p, 1e-5, "adamw")
+
+
+def test_dora_weight_matches_reference_fixture(golden_dir):
+    import vit_amd
+    fx = torch.load(os.path.join(golden_dir, "dora_golden.pt"), weights_only=True)
+    rec = fx["96x80r8"]
+    m = rec["m"].clone().to(DEV).requires_grad_(True)
+    A = rec["A"].clone().to(DEV).requires_grad_(True)
+    Bm = rec["B"].clone().to(DEV).requires_grad_(True)
+    W = vit_amd.dora_weight(m, A, Bm, rec["D"].to(DEV), rec["scaling"])
+    _close(W, rec["W"], 1e-5, "dora W")
+    W.backward(rec["gW"].to(DEV))
+    _close(m.grad, rec["dm"], 1e-4, "dm")
+    _close(A.grad, rec["dA"], 1e-4, "dA")
+    _close(Bm.grad, rec["dB"], 1e-4, "dB")
+    # full-size layers: regenerate inputs from the recorded seed, compare summaries
+    from oracle import vit_ref as R
+    for key in ("1024x1024r32", "768x768r32"):
+        r = fx[key]
+        torch.manual_seed(r["seed"])
+        base = torch.nn.Linear(r["in"], r["out"])
+        layer = vit_amd.DoRALayer(base, r=r["r"], dora_alpha=16)
+        layer = layer.to(DEV)
+        W = layer.weight
+        assert abs(W.double().sum().item() - r["W_sum"]) < 1e-4 * abs(r["W_abs"])
+        _close(W[0, :64], r["W_row0"], 1e-5, "row0")
+        gW = torch.randn(W.shape, generator=torch.Generator().manual_seed(0))  # grads checked on the oracle
+        W.backward(gW.to(DEV))
+        mo = layer.m.detach().cpu().clone().requires_grad_(True)
+        Ao = layer.delta_D_A.detach().cpu().clone().requires_grad_(True)
+        Bo = layer.delta_D_B.detach().cpu().clone().requires_grad_(True)
+        Wo = R.dora_weight(mo, Ao, Bo, layer.D.cpu(), layer.scaling)
+        Wo.backward(gW)
+        _close(layer.m.grad, mo.grad, 1e-4, "dm full")
+        _close(layer.delta_D_A.grad, Ao.grad, 1e-4, "dA full")
+        _close(layer.delta_D_B.grad, Bo.grad, 1e-4, "dB full")

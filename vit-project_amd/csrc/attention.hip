@@ -1,0 +1,508 @@
+// Scaled-dot-product attention for timm Attention: per (batch, head)
+// softmax(q k^T * hd^-0.5) v with no mask, N <= 288 tokens (197 for ViT-B/16,
+// 257 for CLIP ViT-L/14), head_dim 64.
+//
+// q/k/v are read in place from the fused qkv GEMM output [B*N, 3*D] (row stride
+// ld_qkv), the output o is written as [B*N, D] (the proj GEMM operand), and the
+// backward writes dq/dk/dv into a [B*N, 3*D] buffer laid out like qkv so the
+// qkv dgrad/wgrad GEMMs consume it directly.
+//
+// bf16 path: one workgroup (4 waves) per (b, h); the whole K and V of the head
+// live in LDS (<= 2 x 36 KiB); S^T = K Q^T with v_mfma_f32_16x16x32_bf16 so each
+// lane owns one query column and the softmax row-max/row-sum are in-lane plus two
+// cross-lane shuffles; P stays in registers and feeds the PV MFMA as its
+// B-operand (k-slot permutation pi), V^T comes from ds_read_b64_tr_b16.
+// f32 path (parity mode): scalar-FMA online softmax.
+#include "common.hpp"
+
+// 128-B row image with XOR swizzle (row & 6) on 16-B chunks: conflict-free for
+// the 16x16x32 ds_read_b128 fragment reads and for the ds_read_b64_tr_b16 reads
+// of 8 consecutive rows (LDS images).
+__device__ __forceinline__ int at_off(int row, int c) { return row * 128 + ((c ^ (row & 6)) << 4); }
+
+__device__ __forceinline__ bf16x8 at_row_frag(const char* img, int row0, int kk, int lane) {
+  return *reinterpret_cast<const bf16x8*>(img + at_off(row0 + (lane & 15), kk * 4 + (lane >> 4)));
+}
+// transposed fragment: rows (keys/queries) row0 + pi(8g+e), columns d0..d0+15.
+__device__ __forceinline__ bf16x8 at_tr_frag(const char* img, int row0, int d0, int lane) {
+  int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  int c = (d0 >> 3) + (p >> 1);
+  int ra = row0 + 4 * g + q, rb = ra + 16;
+  bf16x4 lo = lds_read_tr(img + at_off(ra, c) + (p & 1) * 8);
+  bf16x4 hi = lds_read_tr(img + at_off(rb, c) + (p & 1) * 8);
+  return cat4(lo, hi);
+}
+
+// Load rows [0, N) of a head's 64-wide slice into an LDS image of `rows` rows,
+// zero-filling rows >= N.
+__device__ __forceinline__ void at_load(char* img, const bf16* src, int64_t ld, int N, int rows) {
+  for (int idx = threadIdx.x; idx < rows * 8; idx += blockDim.x) {
+    int row = idx >> 3, c = idx & 7;
+    bf16x8 v;
+    if (row < N) v = *reinterpret_cast<const bf16x8*>(src + (int64_t)row * ld + c * 8);
+    else { for (int t = 0; t < 8; ++t) v[t] = (bf16)0.f; }
+    *reinterpret_cast<bf16x8*>(img + at_off(row, c)) = v;
+  }
+}
+
+__device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
+  return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+}
+
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+// ---------------------------------------------------------------------------
+// bf16 forward
+// ---------------------------------------------------------------------------
+template <int NT>  // key/query tiles of 16: NT = ceil(N/16)
+__global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D,
+                                                     int H, int N, float scale, bf16* __restrict__ o,
+                                                     int64_t ld_o, float* __restrict__ lse) {
+  constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
+  __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128];
+  char* Kimg = smem;
+  char* Vimg = smem + ROWS * 128;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const bf16* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  at_load(Kimg, base + D, ld_qkv, N, ROWS);
+  at_load(Vimg, base + 2 * D, ld_qkv, N, ROWS);
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  for (int qt = wave; qt < NT; qt += 4) {
+    const int q = qt * 16 + (lane & 15);
+    bf16x8 qf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (q < N) qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)q * ld_qkv + kk * 32 + g * 8);
+      else { for (int t = 0; t < 8; ++t) qf[kk][t] = (bf16)0.f; }
+    }
+    f32x4 s[NT];
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) s[kt] = mfma16(at_row_frag(Kimg, kt * 16, kk, lane), qf[kk], s[kt]);
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int key = kt * 16 + 4 * g + r;
+        float v = (key < N) ? s[kt][r] * c2 : -INFINITY;
+        s[kt][r] = v;
+        m = fmaxf(m, v);
+      }
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { float p = exp2f(s[kt][r] - m); s[kt][r] = p; l += p; }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 oacc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < NT2; ++ks) {
+      f32x4 hi = (2 * ks + 1 < NT) ? s[2 * ks + 1 < NT ? 2 * ks + 1 : 0] : f32x4{0.f, 0.f, 0.f, 0.f};
+      bf16x8 pf = pack8(s[2 * ks], hi);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma16(at_tr_frag(Vimg, ks * 32, dt * 16, lane), pf, oacc[dt]);
+    }
+    if (q < N) {
+      const float inv = 1.0f / l;
+      bf16* orow = o + ((int64_t)b * N + q) * ld_o + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 ov = {(bf16)(oacc[dt][0] * inv), (bf16)(oacc[dt][1] * inv), (bf16)(oacc[dt][2] * inv),
+                     (bf16)(oacc[dt][3] * inv)};
+        *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = ov;
+      }
+      if (g == 0) lse[(int64_t)bh * N + q] = (m + log2f(l)) * LN2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// bf16 backward: phase 1 key-parallel (dK, dV), phase 2 query-parallel (dQ).
+// ---------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(256) void attn_bwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                     int N, float scale, const bf16* __restrict__ o, int64_t ld_o,
+                                                     const bf16* __restrict__ dout, int64_t ld_do,
+                                                     const float* __restrict__ lse, bf16* __restrict__ dqkv,
+                                                     int64_t ld_dqkv) {
+  constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Qimg = smem;
+  char* Kimg = Qimg + ROWS * 128;
+  char* Vimg = Kimg + ROWS * 128;
+  char* Oimg = Vimg + ROWS * 128;  // dO
+  float* lse2 = reinterpret_cast<float*>(Oimg + ROWS * 128);
+  float* delta = lse2 + ROWS;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const bf16* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  const bf16* dob = dout + (int64_t)b * N * ld_do + h * 64;
+  at_load(Qimg, base, ld_qkv, N, ROWS);
+  at_load(Kimg, base + D, ld_qkv, N, ROWS);
+  at_load(Vimg, base + 2 * D, ld_qkv, N, ROWS);
+  at_load(Oimg, dob, ld_do, N, ROWS);
+  // delta[q] = sum_d dO*O (one wave per row, 64 lanes = 64 dims), lse in log2 units
+  for (int q = wave; q < ROWS; q += 4) {
+    float dsum = 0.f;
+    if (q < N) {
+      dsum = (float)dob[(int64_t)q * ld_do + lane] * (float)o[((int64_t)b * N + q) * ld_o + h * 64 + lane];
+      dsum = wave_sum(dsum);
+    }
+    if (lane == 0) {
+      delta[q] = dsum;
+      lse2[q] = (q < N) ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
+    }
+  }
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+
+  // ---- phase 1: key tiles -> dK, dV
+  for (int kt = wave; kt < NT; kt += 4) {
+    const int key = kt * 16 + (lane & 15);
+    bf16x8 kf[2], vf[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      kf[kk] = at_row_frag(Kimg, kt * 16, kk, lane);
+      vf[kk] = at_row_frag(Vimg, kt * 16, kk, lane);
+    }
+    f32x4 dv[4], dk[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) { dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[dt] = dv[dt]; }
+    for (int qp = 0; qp < NT2; ++qp) {
+      f32x4 p[2], ds[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int qt = 2 * qp + u;
+        f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dpacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          sacc = mfma16(at_row_frag(Qimg, qt * 16, kk, lane), kf[kk], sacc);
+          dpacc = mfma16(at_row_frag(Oimg, qt * 16, kk, lane), vf[kk], dpacc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int qq = qt * 16 + 4 * g + r;
+          float pv = (key < N) ? exp2f(sacc[r] * c2 - lse2[qq]) : 0.f;
+          p[u][r] = pv;
+          ds[u][r] = pv * (dpacc[r] - delta[qq]);
+        }
+      }
+      bf16x8 pf = pack8(p[0], p[1]), dsf = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma16(at_tr_frag(Oimg, qp * 32, dt * 16, lane), pf, dv[dt]);
+        dk[dt] = mfma16(at_tr_frag(Qimg, qp * 32, dt * 16, lane), dsf, dk[dt]);
+      }
+    }
+    if (key < N) {
+      bf16* row = dqkv + ((int64_t)b * N + key) * ld_dqkv + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 kv = {(bf16)(dk[dt][0] * scale), (bf16)(dk[dt][1] * scale), (bf16)(dk[dt][2] * scale),
+                     (bf16)(dk[dt][3] * scale)};
+        bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
+        *reinterpret_cast<bf16x4*>(row + D + dt * 16 + 4 * g) = kv;
+        *reinterpret_cast<bf16x4*>(row + 2 * D + dt * 16 + 4 * g) = vv;
+      }
+    }
+  }
+
+  // ---- phase 2: query tiles -> dQ
+  for (int qt = wave; qt < NT; qt += 4) {
+    const int q = qt * 16 + (lane & 15);
+    bf16x8 qf[2], of[2];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[kk] = at_row_frag(Qimg, qt * 16, kk, lane);
+      of[kk] = at_row_frag(Oimg, qt * 16, kk, lane);
+    }
+    const float l2 = lse2[q], dl = delta[q];
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kp = 0; kp < NT2; ++kp) {
+      f32x4 ds[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kt = 2 * kp + u;
+        f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dpacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          sacc = mfma16(at_row_frag(Kimg, kt * 16, kk, lane), qf[kk], sacc);
+          dpacc = mfma16(at_row_frag(Vimg, kt * 16, kk, lane), of[kk], dpacc);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int key = kt * 16 + 4 * g + r;
+          float pv = (key < N) ? exp2f(sacc[r] * c2 - l2) : 0.f;
+          ds[u][r] = pv * (dpacc[r] - dl);
+        }
+      }
+      bf16x8 dsf = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(at_tr_frag(Kimg, kp * 32, dt * 16, lane), dsf, dq[dt]);
+    }
+    if (q < N) {
+      bf16* row = dqkv + ((int64_t)b * N + q) * ld_dqkv + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 qv = {(bf16)(dq[dt][0] * scale), (bf16)(dq[dt][1] * scale), (bf16)(dq[dt][2] * scale),
+                     (bf16)(dq[dt][3] * scale)};
+        *reinterpret_cast<bf16x4*>(row + dt * 16 + 4 * g) = qv;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// generic (f32 compute, f32 or bf16 storage) path: 4 lanes per query / key,
+// each owning 16 of the 64 head dims; keys / queries streamed through LDS.
+// ---------------------------------------------------------------------------
+constexpr int GCH = 64;  // rows per LDS chunk
+
+template <typename T>
+__global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                        int N, float scale, T* __restrict__ o, int64_t ld_o,
+                                                        float* __restrict__ lse) {
+  __shared__ float Ks[GCH][65], Vs[GCH][65];
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int t = threadIdx.x, qi = blockIdx.x * 64 + (t >> 2), u = t & 3;
+  const T* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  float qv[16], acc[16];
+  const bool valid = qi < N;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) { qv[d] = valid ? (float)base[(int64_t)qi * ld_qkv + u * 16 + d] * scale : 0.f; acc[d] = 0.f; }
+  float m = -INFINITY, l = 0.f;
+  for (int j0 = 0; j0 < N; j0 += GCH) {
+    __syncthreads();
+    for (int idx = t; idx < GCH * 64; idx += 256) {
+      int r = idx >> 6, d = idx & 63, j = j0 + r;
+      Ks[r][d] = j < N ? (float)base[(int64_t)j * ld_qkv + D + d] : 0.f;
+      Vs[r][d] = j < N ? (float)base[(int64_t)j * ld_qkv + 2 * D + d] : 0.f;
+    }
+    __syncthreads();
+    const int jn = min(GCH, N - j0);
+    for (int r = 0; r < jn; ++r) {
+      float s = 0.f;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) s = fmaf(qv[d], Ks[r][u * 16 + d], s);
+      s += __shfl_xor(s, 1, 64);
+      s += __shfl_xor(s, 2, 64);
+      float mn = fmaxf(m, s);
+      float corr = __expf(m - mn), p = __expf(s - mn);
+      l = l * corr + p;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) acc[d] = acc[d] * corr + p * Vs[r][u * 16 + d];
+      m = mn;
+    }
+  }
+  if (!valid) return;
+  const float inv = 1.f / l;
+  T* orow = o + ((int64_t)b * N + qi) * ld_o + h * 64 + u * 16;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) orow[d] = (T)(acc[d] * inv);
+  if (u == 0) lse[(int64_t)bh * N + qi] = m + logf(l);
+}
+
+// q-parallel: delta_i = dO_i . O_i ; dQ_i = scale * sum_j p_ij (dO_i.v_j - delta_i) k_j
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_dq_generic(const T* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                           int N, float scale, const T* __restrict__ o,
+                                                           int64_t ld_o, const T* __restrict__ dout, int64_t ld_do,
+                                                           const float* __restrict__ lse, float* __restrict__ delta_out,
+                                                           T* __restrict__ dqkv, int64_t ld_dqkv) {
+  __shared__ float Ks[GCH][65], Vs[GCH][65];
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int t = threadIdx.x, qi = blockIdx.x * 64 + (t >> 2), u = t & 3;
+  const T* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  const bool valid = qi < N;
+  float qv[16], dov[16], acc[16];
+  float dl = 0.f;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    qv[d] = valid ? (float)base[(int64_t)qi * ld_qkv + u * 16 + d] * scale : 0.f;
+    dov[d] = valid ? (float)dout[((int64_t)b * N + qi) * ld_do + h * 64 + u * 16 + d] : 0.f;
+    float ov = valid ? (float)o[((int64_t)b * N + qi) * ld_o + h * 64 + u * 16 + d] : 0.f;
+    dl = fmaf(dov[d], ov, dl);
+    acc[d] = 0.f;
+  }
+  dl += __shfl_xor(dl, 1, 64);
+  dl += __shfl_xor(dl, 2, 64);
+  const float L = valid ? lse[(int64_t)bh * N + qi] : 0.f;
+  for (int j0 = 0; j0 < N; j0 += GCH) {
+    __syncthreads();
+    for (int idx = t; idx < GCH * 64; idx += 256) {
+      int r = idx >> 6, d = idx & 63, j = j0 + r;
+      Ks[r][d] = j < N ? (float)base[(int64_t)j * ld_qkv + D + d] : 0.f;
+      Vs[r][d] = j < N ? (float)base[(int64_t)j * ld_qkv + 2 * D + d] : 0.f;
+    }
+    __syncthreads();
+    const int jn = min(GCH, N - j0);
+    for (int r = 0; r < jn; ++r) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) { s = fmaf(qv[d], Ks[r][u * 16 + d], s); dp = fmaf(dov[d], Vs[r][u * 16 + d], dp); }
+      s += __shfl_xor(s, 1, 64); s += __shfl_xor(s, 2, 64);
+      dp += __shfl_xor(dp, 1, 64); dp += __shfl_xor(dp, 2, 64);
+      float ds = __expf(s - L) * (dp - dl);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) acc[d] = fmaf(ds, Ks[r][u * 16 + d], acc[d]);
+    }
+  }
+  if (!valid) return;
+  if (u == 0) delta_out[(int64_t)bh * N + qi] = dl;
+  T* row = dqkv + ((int64_t)b * N + qi) * ld_dqkv + h * 64 + u * 16;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) row[d] = (T)(acc[d] * scale);
+}
+
+// key-parallel: dV_j = sum_i p_ij dO_i ; dK_j = scale * sum_i ds_ij q_i
+template <typename T>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_generic(const T* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                            int N, float scale, const T* __restrict__ dout,
+                                                            int64_t ld_do, const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, T* __restrict__ dqkv,
+                                                            int64_t ld_dqkv) {
+  __shared__ float Qs[GCH][65], Os[GCH][65];
+  __shared__ float Ls[GCH], Dl[GCH];
+  const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
+  const int t = threadIdx.x, kj = blockIdx.x * 64 + (t >> 2), u = t & 3;
+  const T* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  const bool valid = kj < N;
+  float kv[16], vv[16], dk[16], dv[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    kv[d] = valid ? (float)base[(int64_t)kj * ld_qkv + D + u * 16 + d] : 0.f;
+    vv[d] = valid ? (float)base[(int64_t)kj * ld_qkv + 2 * D + u * 16 + d] : 0.f;
+    dk[d] = 0.f; dv[d] = 0.f;
+  }
+  for (int i0 = 0; i0 < N; i0 += GCH) {
+    __syncthreads();
+    for (int idx = t; idx < GCH * 64; idx += 256) {
+      int r = idx >> 6, d = idx & 63, i = i0 + r;
+      Qs[r][d] = i < N ? (float)base[(int64_t)i * ld_qkv + d] : 0.f;
+      Os[r][d] = i < N ? (float)dout[((int64_t)b * N + i) * ld_do + h * 64 + d] : 0.f;
+    }
+    if (t < GCH) {
+      int i = i0 + t;
+      Ls[t] = i < N ? lse[(int64_t)bh * N + i] : 0.f;
+      Dl[t] = i < N ? delta[(int64_t)bh * N + i] : 0.f;
+    }
+    __syncthreads();
+    const int in = min(GCH, N - i0);
+    for (int r = 0; r < in; ++r) {
+      float s = 0.f, dp = 0.f;
+#pragma unroll
+      for (int d = 0; d < 16; ++d) { s = fmaf(Qs[r][u * 16 + d], kv[d], s); dp = fmaf(Os[r][u * 16 + d], vv[d], dp); }
+      s += __shfl_xor(s, 1, 64); s += __shfl_xor(s, 2, 64);
+      dp += __shfl_xor(dp, 1, 64); dp += __shfl_xor(dp, 2, 64);
+      float p = __expf(s * scale - Ls[r]);
+      float ds = p * (dp - Dl[r]);
+#pragma unroll
+      for (int d = 0; d < 16; ++d) { dv[d] = fmaf(p, Os[r][u * 16 + d], dv[d]); dk[d] = fmaf(ds, Qs[r][u * 16 + d], dk[d]); }
+    }
+  }
+  if (!valid) return;
+  T* row = dqkv + ((int64_t)b * N + kj) * ld_dqkv + h * 64 + u * 16;
+#pragma unroll
+  for (int d = 0; d < 16; ++d) { row[D + d] = (T)(dk[d] * scale); row[2 * D + d] = (T)dv[d]; }
+}
+
+// ---------------------------------------------------------------------------
+template <int NT>
+static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, void* o,
+                    int64_t ld_o, float* lse, hipStream_t s) {
+  hipLaunchKernelGGL((attn_fwd_mfma<NT>), dim3(B * H), dim3(256), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
+                     (bf16*)o, ld_o, lse);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+template <int NT>
+static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, const void* o,
+                    int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
+                    hipStream_t s) {
+  constexpr int ROWS = ((NT + 1) / 2) * 32;
+  size_t lds = 4 * ROWS * 128 + 2 * ROWS * sizeof(float);
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_mfma<NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((attn_bwd_mfma<NT>), dim3(B * H), dim3(256), lds, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
+                     (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, (bf16*)dqkv, ld_dqkv);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+#define NT_CASES(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18)
+
+extern "C" {
+
+// F.scaled_dot_product_attention(q, k, v) (no mask, no dropout) for head_dim 64.
+// qkv: [B*N, ld_qkv] with q at column h*64, k at D + h*64, v at 2D + h*64.
+// o: [B*N, ld_o] (column h*64); lse: [B*H*N] f32 (natural-log, scaled scores).
+int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, void* o,
+                 int64_t ld_o, float* lse, float scale, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (head_dim != 64 || N <= 0 || N > 288) return (int)hipErrorInvalidValue;
+  const int D = H * 64;
+  if (dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_o % 4 == 0)) {
+    int nt = (N + 15) / 16;
+    switch (nt) {
+#define CASE(n) case n: return fwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, lse, s);
+      NT_CASES(CASE)
+#undef CASE
+    }
+  }
+  dim3 grid((N + 63) / 64, B * H);
+  if (dtype == VIT_BF16)
+    hipLaunchKernelGGL(attn_fwd_generic<bf16>, grid, dim3(256), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale, (bf16*)o, ld_o, lse);
+  else
+    hipLaunchKernelGGL(attn_fwd_generic<float>, grid, dim3(256), 0, s, (const float*)qkv, ld_qkv, D, H, N, scale, (float*)o, ld_o, lse);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+// SDPA backward: writes dq/dk/dv into dqkv (same column layout as qkv).
+// `delta_ws` (>= B*H*N floats) is scratch for the generic path (may be null on the bf16 path).
+int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, const void* o,
+                 int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
+                 float* delta_ws, float scale, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (head_dim != 64 || N <= 0 || N > 288) return (int)hipErrorInvalidValue;
+  const int D = H * 64;
+  if (dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_do % 8 == 0) && (ld_dqkv % 4 == 0)) {
+    int nt = (N + 15) / 16;
+    switch (nt) {
+#define CASE(n) case n: return bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, dout, ld_do, lse, dqkv, ld_dqkv, s);
+      NT_CASES(CASE)
+#undef CASE
+    }
+  }
+  if (!delta_ws) return (int)hipErrorInvalidValue;
+  dim3 grid((N + 63) / 64, B * H);
+#define GEN(T)                                                                                               \
+  hipLaunchKernelGGL(attn_bwd_dq_generic<T>, grid, dim3(256), 0, s, (const T*)qkv, ld_qkv, D, H, N, scale,    \
+                     (const T*)o, ld_o, (const T*)dout, ld_do, lse, delta_ws, (T*)dqkv, ld_dqkv);            \
+  VIT_CHECK_LAUNCH();                                                                                        \
+  hipLaunchKernelGGL(attn_bwd_dkv_generic<T>, grid, dim3(256), 0, s, (const T*)qkv, ld_qkv, D, H, N, scale,   \
+                     (const T*)dout, ld_do, lse, delta_ws, (T*)dqkv, ld_dqkv);
+  if (dtype == VIT_BF16) { GEN(bf16) } else { GEN(float) }
+#undef GEN
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,277 @@
+// LayerNorm over the last dim (timm norm1/norm2/norm, eps 1e-6; CLIP eps 1e-5).
+// One wave per row.  Forward: biased variance, two-pass in registers, saves
+// mean/rstd.  Backward: dx = rstd*(g - mean(g) - xhat*mean(g*xhat)), g = dy*gamma,
+// plus a fused residual-gradient add and an optional typed copy of dx (the next
+// GEMM operand, optionally with the CLS rows dropped); dgamma/dbeta via
+// per-block partials + a final reduce.
+//
+// NV = float4 groups per lane (D = 256*NV: 3 for ViT-B's 768, 4 for 1024); a
+// scalar kernel (NV = 0) covers any other D (test configs).
+#include "common.hpp"
+
+constexpr int LN_WAVES = 4;   // rows per block in the forward (one per wave)
+constexpr int LN_SMAX = 32;   // scalar path: D <= 64*32
+
+template <typename T> __device__ __forceinline__ f32x4 ld4(const T* p);
+template <> __device__ __forceinline__ f32x4 ld4<float>(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+template <> __device__ __forceinline__ f32x4 ld4<bf16>(const bf16* p) {
+  bf16x4 x = *reinterpret_cast<const bf16x4*>(p);
+  return f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+}
+template <typename T> __device__ __forceinline__ void st4(T* p, f32x4 v);
+template <> __device__ __forceinline__ void st4<float>(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+template <> __device__ __forceinline__ void st4<bf16>(bf16* p, f32x4 v) {
+  *reinterpret_cast<bf16x4*>(p) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+}
+
+// first column of float4 group k of this lane
+__device__ __forceinline__ int col4(int lane, int k) { return (k * 64 + lane) * 4; }
+
+template <int NV, typename TX, typename TY>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, int64_t ldx, TY* __restrict__ y,
+                                                     int64_t ldy, const float* __restrict__ w,
+                                                     const float* __restrict__ b, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, int rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const TX* xr = x + (int64_t)row * ldx;
+  TY* yr = y + (int64_t)row * ldy;
+  if constexpr (NV > 0) {
+    f32x4 v[NV];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) { v[k] = ld4<TX>(xr + col4(lane, k)); s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]); }
+    const float mu = wave_sum(s) / D;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) { float d = v[k][t] - mu; q += d * d; }
+    const float rs = rsqrtf(wave_sum(q) / D + eps);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      int c = col4(lane, k);
+      f32x4 g = *reinterpret_cast<const f32x4*>(w + c), bb = *reinterpret_cast<const f32x4*>(b + c), o;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = (v[k][t] - mu) * rs * g[t] + bb[t];
+      st4<TY>(yr + c, o);
+    }
+    if (lane == 0) { if (mean) mean[row] = mu; if (rstd) rstd[row] = rs; }
+  } else {
+    float s = 0.f;
+    for (int c = lane; c < D; c += 64) s += (float)xr[c];
+    const float mu = wave_sum(s) / D;
+    float q = 0.f;
+    for (int c = lane; c < D; c += 64) { float d = (float)xr[c] - mu; q += d * d; }
+    const float rs = rsqrtf(wave_sum(q) / D + eps);
+    for (int c = lane; c < D; c += 64) yr[c] = (TY)(((float)xr[c] - mu) * rs * w[c] + b[c]);
+    if (lane == 0) { if (mean) mean[row] = mu; if (rstd) rstd[row] = rs; }
+  }
+}
+
+__device__ __forceinline__ bool copy_row(int row, int compact_np, int64_t& orow) {
+  orow = row;
+  if (compact_np > 0) {
+    int bb = row / (compact_np + 1), p = row - bb * (compact_np + 1);
+    orow = (int64_t)bb * compact_np + p - 1;
+    return p != 0;
+  }
+  return true;
+}
+
+// Backward: block = 4 waves over rows [blk*rows_per, ...), wave-strided.
+template <int NV, typename TX, typename TD, typename TC>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(
+    const TX* __restrict__ x, int64_t ldx, const TD* __restrict__ dy, int64_t lddy,
+    const float* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ dres, int64_t ldres, float* __restrict__ dx, int64_t lddx,
+    TC* __restrict__ dxc, int64_t ldc, int compact_np, float* __restrict__ part_g,
+    float* __restrict__ part_b, int rows, int D, int rows_per) {
+  constexpr int NP = NV > 0 ? NV * 4 : LN_SMAX;  // partial slots per lane
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  float pg[NP], pb[NP];
+#pragma unroll
+  for (int t = 0; t < NP; ++t) { pg[t] = 0.f; pb[t] = 0.f; }
+  __shared__ float red[LN_WAVES][128];
+  const int r0 = blockIdx.x * rows_per, r1 = min(rows, r0 + rows_per);
+  for (int row = r0 + wv; row < r1; row += LN_WAVES) {
+    const TX* xr = x + (int64_t)row * ldx;
+    const TD* dyr = dy + (int64_t)row * lddy;
+    const float mu = mean[row], rs = rstd[row];
+    float* dxr = dx + (int64_t)row * lddx;
+    int64_t orow = row;
+    const bool keep = (dxc != nullptr) && copy_row(row, compact_np, orow);
+    if constexpr (NV > 0) {
+      f32x4 xh[NV], g[NV];
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        int c = col4(lane, k);
+        f32x4 xv = ld4<TX>(xr + c), dv = ld4<TD>(dyr + c), wv4 = *reinterpret_cast<const f32x4*>(w + c);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          xh[k][t] = (xv[t] - mu) * rs;
+          g[k][t] = dv[t] * wv4[t];
+          s1 += g[k][t];
+          s2 += g[k][t] * xh[k][t];
+          pg[k * 4 + t] += dv[t] * xh[k][t];
+          pb[k * 4 + t] += dv[t];
+        }
+      }
+      s1 = wave_sum(s1) / D;
+      s2 = wave_sum(s2) / D;
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        int c = col4(lane, k);
+        f32x4 o;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) o[t] = rs * (g[k][t] - s1 - xh[k][t] * s2);
+        if (dres) o += *reinterpret_cast<const f32x4*>(dres + (int64_t)row * ldres + c);
+        *reinterpret_cast<f32x4*>(dxr + c) = o;
+        if (keep) st4<TC>(dxc + orow * ldc + c, o);
+      }
+    } else {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int k = 0; k < LN_SMAX; ++k) {
+        int c = lane + 64 * k;
+        if (c < D) {
+          float xh = ((float)xr[c] - mu) * rs, dv = (float)dyr[c], g = dv * w[c];
+          s1 += g; s2 += g * xh;
+          pg[k] += dv * xh; pb[k] += dv;
+        }
+      }
+      s1 = wave_sum(s1) / D;
+      s2 = wave_sum(s2) / D;
+      for (int c = lane; c < D; c += 64) {
+        float xh = ((float)xr[c] - mu) * rs, g = (float)dyr[c] * w[c];
+        float o = rs * (g - s1 - xh * s2);
+        if (dres) o += dres[(int64_t)row * ldres + c];
+        dxr[c] = o;
+        if (keep) dxc[orow * ldc + c] = (TC)o;
+      }
+    }
+  }
+  if (!part_g) return;
+  float* out_g = part_g + (int64_t)blockIdx.x * D;
+  float* out_b = part_b + (int64_t)blockIdx.x * D;
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int c = NV > 0 ? col4(lane, k >> 2) + (k & 3) : k * 64 + lane;
+    if (NV == 0 && k * 64 >= D) break;  // uniform across the block
+    red[wv][lane] = pg[k];
+    red[wv][64 + lane] = pb[k];
+    __syncthreads();
+    if (wv == 0 && c < D) {
+      out_g[c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+      out_b[c] = (red[0][64 + lane] + red[1][64 + lane]) + (red[2][64 + lane] + red[3][64 + lane]);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void partial_reduce_kernel(const float* __restrict__ part, int S, int D, float* __restrict__ out) {
+  int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= D) return;
+  float s = 0.f;
+  for (int z = 0; z < S; ++z) s += part[(int64_t)z * D + c];
+  out[c] = s;
+}
+
+template <typename TX, typename TY>
+static void launch_fwd(int nv, dim3 grid, hipStream_t s, const void* x, int64_t ldx, void* y, int64_t ldy,
+                       const float* w, const float* b, float* mean, float* rstd, int rows, int D, float eps) {
+#define F(NV) hipLaunchKernelGGL((ln_fwd_kernel<NV, TX, TY>), grid, dim3(64 * LN_WAVES), 0, s, (const TX*)x, ldx, (TY*)y, ldy, w, b, mean, rstd, rows, D, eps)
+  switch (nv) {
+    case 1: F(1); break;
+    case 2: F(2); break;
+    case 3: F(3); break;
+    case 4: F(4); break;
+    case 6: F(6); break;
+    case 8: F(8); break;
+    default: F(0); break;
+  }
+#undef F
+}
+
+template <typename TX, typename TD, typename TC>
+static void launch_bwd(int nv, int nblk, hipStream_t s, const void* x, int64_t ldx, const void* dy, int64_t lddy,
+                       const float* w, const float* mean, const float* rstd, const float* dres, int64_t ldres,
+                       float* dx, int64_t lddx, void* dxc, int64_t ldc, int compact_np, float* pg, float* pb,
+                       int rows, int D, int rows_per) {
+#define B(NV) hipLaunchKernelGGL((ln_bwd_kernel<NV, TX, TD, TC>), dim3(nblk), dim3(64 * LN_WAVES), 0, s, (const TX*)x, ldx, \
+                                 (const TD*)dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, (TC*)dxc, ldc, compact_np, pg, pb, rows, D, rows_per)
+  switch (nv) {
+    case 3: B(3); break;
+    case 4: B(4); break;
+    default: B(0); break;
+  }
+#undef B
+}
+
+extern "C" {
+
+// F.layer_norm forward over rows of x (row stride ldx; f32 or bf16 in) -> y (dtype_y).
+int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x, int64_t ldx, void* y,
+                       int64_t ldy, const float* w, const float* b, float* mean, float* rstd, float eps,
+                       void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (rows <= 0) return 0;
+  if (D > 64 * LN_SMAX) return (int)hipErrorInvalidValue;
+  dim3 grid((rows + LN_WAVES - 1) / LN_WAVES);
+  bool vec = (D % 256 == 0) && (ldx % 4 == 0) && (ldy % 4 == 0);
+  int nv = vec ? D / 256 : 0;
+  if (dtype_x == VIT_F32 && dtype_y == VIT_F32) launch_fwd<float, float>(nv, grid, s, x, ldx, y, ldy, w, b, mean, rstd, rows, D, eps);
+  else if (dtype_x == VIT_F32) launch_fwd<float, bf16>(nv, grid, s, x, ldx, y, ldy, w, b, mean, rstd, rows, D, eps);
+  else if (dtype_y == VIT_BF16) launch_fwd<bf16, bf16>(nv, grid, s, x, ldx, y, ldy, w, b, mean, rstd, rows, D, eps);
+  else launch_fwd<bf16, float>(nv, grid, s, x, ldx, y, ldy, w, b, mean, rstd, rows, D, eps);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+// LayerNorm backward.  dx (f32) = dres + LN'(dy).  dx_copy (optional, dtype_copy,
+// row stride ld_copy) is the GEMM-operand copy of dx; compact_np > 0 drops the
+// CLS row of every (compact_np+1)-row image (patch-embed wgrad operand).
+// dgamma/dbeta (may be null) need `partial` >= 2*nblk*D floats, nblk = ceil(rows/rows_per).
+int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x, int64_t ldx,
+                       const void* dy, int64_t lddy, const float* w, const float* mean, const float* rstd,
+                       const float* dres, int64_t ldres, float* dx, int64_t lddx, void* dx_copy, int64_t ld_copy,
+                       int dtype_copy, int compact_np, float* dgamma, float* dbeta, float* partial,
+                       int64_t partial_floats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (rows <= 0) return 0;
+  if (D > 64 * LN_SMAX) return (int)hipErrorInvalidValue;
+  int rows_per = 64;
+  int nblk = (rows + rows_per - 1) / rows_per;
+  if (dgamma) {
+    while ((int64_t)2 * nblk * D > partial_floats && rows_per < rows) {
+      rows_per *= 2;
+      nblk = (rows + rows_per - 1) / rows_per;
+    }
+    if ((int64_t)2 * nblk * D > partial_floats) return (int)hipErrorInvalidValue;
+  }
+  float* pg = dgamma ? partial : nullptr;
+  float* pb = dgamma ? partial + (int64_t)nblk * D : nullptr;
+  bool vec = (D % 256 == 0) && (ldx % 4 == 0) && (lddy % 4 == 0) && (lddx % 4 == 0) && (ldres % 4 == 0) &&
+             (ld_copy % 4 == 0);
+  int nv = vec ? D / 256 : 0;
+#define LB(TX, TD) \
+  if (dtype_copy == VIT_BF16) launch_bwd<TX, TD, bf16>(nv, nblk, s, x, ldx, dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, dx_copy, ld_copy, compact_np, pg, pb, rows, D, rows_per); \
+  else launch_bwd<TX, TD, float>(nv, nblk, s, x, ldx, dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, dx_copy, ld_copy, compact_np, pg, pb, rows, D, rows_per);
+  if (dtype_x == VIT_F32 && dtype_dy == VIT_F32) { LB(float, float) }
+  else if (dtype_x == VIT_F32) { LB(float, bf16) }
+  else if (dtype_dy == VIT_BF16) { LB(bf16, bf16) }
+  else { LB(bf16, float) }
+#undef LB
+  VIT_CHECK_LAUNCH();
+  if (dgamma) {
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((D + 255) / 256), dim3(256), 0, s, pg, nblk, D, dgamma);
+    VIT_CHECK_LAUNCH();
+    hipLaunchKernelGGL(partial_reduce_kernel, dim3((D + 255) / 256), dim3(256), 0, s, pb, nblk, D, dbeta);
+    VIT_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+}  // extern "C"

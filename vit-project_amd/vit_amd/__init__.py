@@ -1,0 +1,17 @@
+"""vit_amd: MI355X-native (gfx950) ViT training step behind the timm / DoRA surface.
+
+Compute runs only in ``lib/libvit_hip.so`` (C-ABI, include/vit_hip.h); this
+package is the host-side mirror of the reference's module/optimizer interface.
+"""
+from . import _lib
+from .model import VisionTransformer, create_model, cross_entropy
+from .optim import FusedSGD, FusedAdamW, CosineAnnealingLRWithWarmup
+from .dora import DoRALayer, dora_weight
+from . import rsa
+
+__all__ = ["VisionTransformer", "create_model", "cross_entropy", "FusedSGD", "FusedAdamW",
+           "CosineAnnealingLRWithWarmup", "DoRALayer", "dora_weight", "rsa"]
+
+
+def load_library(path=None):
+    return _lib.load(path)

@@ -1,0 +1,434 @@
+"""ViT-B/16 behind timm's ``VisionTransformer`` surface, computed by HIP kernels.
+
+Drop-in for ``timm.create_model('vit_base_patch16_224', pretrained=False,
+num_classes=1000)`` as the reference uses it (VIT:283-287, MEAS:467-485):
+``model(images)`` -> logits, ``model.forward_features(images)`` -> post-norm
+tokens, ``model.global_pool == 'token'``, timm state_dict key names, ``.train()``
+/ ``.eval()``, ``parameters()`` for the optimizer, DDP-compatible autograd.
+
+Master parameters are fp32 ``nn.Parameter``s (what the optimizer and checkpoints
+see).  In ``compute_dtype=torch.bfloat16`` (the performance path) every GEMM
+weight has a bf16 shadow copy that :class:`vit_amd.optim.FusedSGD` refreshes in
+the same pass as the update; any other writer (torch optimizers,
+``load_state_dict``) bumps ``param._version`` and the shadow is recast before
+the next forward.  ``compute_dtype=torch.float32`` is the parity path (generic
+fp32 kernels, 1e-3 relative vs the CPU oracle).
+
+Each transformer block is one autograd node (:class:`_BlockFn`), so the
+backward chains HIP kernels without any torch elementwise glue: residual
+gradients are fused into the LayerNorm backward, GELU' into the fc2 dgrad
+epilogue, bias grads into column-sum kernels.
+"""
+from __future__ import annotations
+
+import math
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+
+from . import _lib as L
+from . import ops
+
+# gradient side channel: a block's backward leaves the GEMM-dtype copy of the
+# residual gradient it produced, keyed by the f32 tensor's storage pointer, for
+# the next (earlier) block's backward to pick up instead of re-casting.
+_GRAD_COPY = {}
+
+
+def _take_copy(g: torch.Tensor, dtype):
+    key = (g.data_ptr(), g.numel())
+    c = _GRAD_COPY.pop(key, None)
+    if c is not None and c[1] == g._version and c[0].dtype == dtype:
+        return c[0]
+    if dtype == torch.float32:
+        return g
+    out = torch.empty(g.shape, dtype=dtype, device=g.device)
+    ops.cast_bf16(g.contiguous(), out)
+    return out
+
+
+def _put_copy(g: torch.Tensor, copy: torch.Tensor):
+    _GRAD_COPY[(g.data_ptr(), g.numel())] = (copy, g._version)
+
+
+class _Shadowed:
+    """Registry of bf16 shadows for GEMM weights."""
+
+    def __init__(self):
+        self.pairs = []  # (param, shadow)
+
+    def add(self, p: nn.Parameter, dtype):
+        if dtype == torch.float32:
+            p._vit_shadow = None
+            return
+        sh = torch.empty(p.shape, dtype=dtype, device=p.device)
+        p._vit_shadow = sh
+        p._vit_shadow_version = -1
+        self.pairs.append(p)
+
+    def refresh(self):
+        for p in self.pairs:
+            if p._vit_shadow.device != p.device or p._vit_shadow.shape != p.shape:
+                p._vit_shadow = torch.empty(p.shape, dtype=p._vit_shadow.dtype, device=p.device)
+                p._vit_shadow_version = -1
+            if p._vit_shadow_version != p._version:
+                ops.cast_bf16(p.detach(), p._vit_shadow)
+                p._vit_shadow_version = p._version
+
+
+def _gout(p: nn.Parameter) -> torch.Tensor:
+    """Where a parameter's gradient is written: its slice of the model's flat
+    gradient buffer (fixed addresses: one all-reduce, a static optimizer table,
+    graph-capture friendly) unless a previous gradient still lives there (then a
+    fresh tensor, so autograd's accumulation stays correct)."""
+    fb = getattr(p, "_vit_flat_grad", None)
+    if fb is not None and (p.grad is None or p.grad.data_ptr() != fb.data_ptr()):
+        return fb
+    return torch.empty(p.shape, dtype=torch.float32, device=p.device)
+
+
+def _w(p: nn.Parameter):
+    sh = getattr(p, "_vit_shadow", None)
+    return p.detach() if sh is None else sh
+
+
+# ----------------------------------------------------------------------------
+# autograd nodes
+# ----------------------------------------------------------------------------
+
+class _PatchEmbedFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, img, w, b, cls, pos, cfg):
+        ctx.params = (w, b, cls, pos)
+        ps, T = cfg["patch"], cfg["dtype"]
+        B = img.shape[0]
+        U = ops.patch_unfold(img.contiguous(), ps, T)
+        npatch = U.shape[0] // B
+        D = w.shape[0]
+        x = ops.patch_embed_fwd(U, _w(w).reshape(D, -1), b.detach(), pos.detach().reshape(-1, D),
+                                cls.detach().reshape(-1), B, npatch)
+        ctx.save_for_backward(U)
+        ctx.meta = (B, npatch, D, tuple(w.shape), T)
+        return x
+
+    @staticmethod
+    def backward(ctx, dx):
+        (U,) = ctx.saved_tensors
+        B, npatch, D, wshape, T = ctx.meta
+        dx = dx.contiguous()
+        S = npatch + 1
+        key = (dx.data_ptr(), dx.numel())
+        c = _GRAD_COPY.pop(key, None)
+        if c is not None and c[1] == dx._version and c[0].dtype == T and c[0].shape[0] == B * npatch:
+            dxc = c[0]
+        else:  # compact copy of the patch rows
+            rows = dx.reshape(B, S, D)[:, 1:, :].reshape(B * npatch, D)
+            if T == torch.float32:
+                dxc = rows.contiguous()
+            else:
+                dxc = torch.empty(B * npatch, D, dtype=T, device=dx.device)
+                ops.cast_bf16(rows.contiguous(), dxc)
+        pw, pb, pc, pp = ctx.params
+        dw = _gout(pw)
+        ops.linear_wgrad(dxc, U, out=dw.view(D, -1))
+        db = ops.colsum(dxc, out=_gout(pb))
+        dpos, dcls = _gout(pp), _gout(pc)
+        ops.pos_grad(dx, B, S, D, dpos, dcls)
+        return None, dw, db, dcls, dpos, None
+
+
+class _BlockFn(torch.autograd.Function):
+    """timm Block: x += proj(sdpa(qkv(norm1(x)))); x += fc2(gelu(fc1(norm2(x))))."""
+
+    @staticmethod
+    def forward(ctx, x, n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b, cfg):
+        B, N, D = x.shape
+        H, T, eps = cfg["heads"], cfg["dtype"], cfg["eps"]
+        act_epi = L.EPI_BIAS_QGELU if cfg["quick_gelu"] else L.EPI_BIAS_GELU
+        M = B * N
+        x2 = x.reshape(M, D)
+        h1, m1, r1 = ops.layer_norm_fwd(x2, n1w.detach(), n1b.detach(), eps, T)
+        qkv = ops.linear_fwd(h1, _w(qkvw), qkvb.detach())
+        o, lse = ops.sdpa_fwd(qkv, B, H, N)
+        xm = ops.linear_fwd(o, _w(projw), projb.detach(), epi=L.EPI_RESID, resid=x2)
+        h2, m2, r2 = ops.layer_norm_fwd(xm, n2w.detach(), n2b.detach(), eps, T)
+        pre, act = ops.linear_fwd(h2, _w(fc1w), fc1b.detach(), epi=act_epi)
+        xo = ops.linear_fwd(act, _w(fc2w), fc2b.detach(), epi=L.EPI_RESID, resid=xm)
+        ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, pre, act)
+        ctx.params = (n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
+        ctx.meta = (B, N, D, H, T, cfg.get("compact_np", 0), cfg["quick_gelu"])
+        return xo.reshape(B, N, D)
+
+    @staticmethod
+    def backward(ctx, dxo):
+        x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, pre, act = ctx.saved_tensors
+        n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b = ctx.params
+        B, N, D, H, T, compact_np, qg = ctx.meta
+        M = B * N
+        dxo = dxo.contiguous().reshape(M, D)
+        dxo_c = _take_copy(dxo, T)
+        gelu_bwd = L.EPI_QGELU_BWD if qg else L.EPI_GELU_BWD
+        # MLP
+        dpre = ops.linear_dgrad(dxo_c, _w(fc2w), out_dtype=T, epi=gelu_bwd, pre=pre)
+        d_fc2w = ops.linear_wgrad(dxo_c, act, out=_gout(fc2w))
+        d_fc2b = ops.colsum(dxo_c, out=_gout(fc2b))
+        dh2 = ops.linear_dgrad(dpre, _w(fc1w), out_dtype=torch.float32)
+        d_fc1w = ops.linear_wgrad(dpre, h2, out=_gout(fc1w))
+        d_fc1b = ops.colsum(dpre, out=_gout(fc1b))
+        dxm = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
+        dxm_c = dxm if T == torch.float32 else torch.empty(M, D, dtype=T, device=dxo.device)
+        d_n2w, d_n2b = _gout(n2w), _gout(n2b)
+        ops.layer_norm_bwd(xm, D, dh2, n2w.detach(), m2, r2, dxm, D, M, dres=dxo, ldres=D,
+                           dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=d_n2w, dbeta=d_n2b)
+        # attention
+        do = ops.linear_dgrad(dxm_c, _w(projw), out_dtype=T)
+        d_projw = ops.linear_wgrad(dxm_c, o, out=_gout(projw))
+        d_projb = ops.colsum(dxm_c, out=_gout(projb))
+        dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N)
+        dh1 = ops.linear_dgrad(dqkv, _w(qkvw), out_dtype=torch.float32)
+        d_qkvw = ops.linear_wgrad(dqkv, h1, out=_gout(qkvw))
+        d_qkvb = ops.colsum(dqkv, out=_gout(qkvb))
+        dx = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
+        d_n1w, d_n1b = _gout(n1w), _gout(n1b)
+        if compact_np:
+            dx_c = torch.empty(B * compact_np, D, dtype=T, device=dxo.device)
+        else:
+            dx_c = None if T == torch.float32 else torch.empty(M, D, dtype=T, device=dxo.device)
+        ops.layer_norm_bwd(x2, D, dh1, n1w.detach(), m1, r1, dx, D, M, dres=dxm, ldres=D, dx_copy=dx_c, ld_copy=D,
+                           compact_np=compact_np, dgamma=d_n1w, dbeta=d_n1b)
+        if dx_c is not None:
+            _put_copy(dx, dx_c)
+        return (dx.reshape(B, N, D), d_n1w, d_n1b, d_qkvw, d_qkvb, d_projw, d_projb, d_n2w, d_n2b, d_fc1w,
+                d_fc1b, d_fc2w, d_fc2b, None)
+
+
+class _HeadFn(torch.autograd.Function):
+    """final norm on the CLS rows only (global_pool='token') + classifier head, f32."""
+
+    @staticmethod
+    def forward(ctx, x, nw, nb, hw, hb, cfg):
+        B, N, D = x.shape
+        xc, mc, rc = ops.layer_norm_fwd(x, nw.detach(), nb.detach(), cfg["eps"], torch.float32, rows=B, ldx=N * D)
+        logits = ops.linear_fwd(xc, hw.detach(), hb.detach(), out_dtype=torch.float32)
+        ctx.save_for_backward(x, xc, mc, rc)
+        ctx.params = (nw, nb, hw, hb)
+        ctx.meta = (B, N, D, cfg["dtype"])
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        x, xc, mc, rc = ctx.saved_tensors
+        nw, nb, hw, hb = ctx.params
+        B, N, D, T = ctx.meta
+        dlogits = dlogits.contiguous().to(torch.float32)
+        dxc = ops.linear_dgrad(dlogits, hw.detach(), out_dtype=torch.float32)
+        dhw = ops.linear_wgrad(dlogits, xc, out=_gout(hw))
+        dhb = ops.colsum(dlogits, out=_gout(hb))
+        dx = ops.zero_(torch.empty(B, N, D, dtype=torch.float32, device=x.device))
+        dx_c = None
+        if T != torch.float32:
+            dx_c = ops.zero_(torch.empty(B * N, D, dtype=T, device=x.device))
+        dnw, dnb = _gout(nw), _gout(nb)
+        ops.layer_norm_bwd(x, N * D, dxc, nw.detach(), mc, rc, dx, N * D, B, dx_copy=dx_c, ld_copy=N * D,
+                           dgamma=dnw, dbeta=dnb)
+        if dx_c is not None:
+            _put_copy(dx, dx_c)
+        return dx, dnw, dnb, dhw, dhb, None
+
+
+class _CrossEntropyFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, target):
+        logits = logits.contiguous().to(torch.float32)
+        loss, row_lse = ops.cross_entropy_fwd(logits, target.contiguous())
+        ctx.save_for_backward(logits, target, row_lse)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, target, row_lse = ctx.saved_tensors
+        return ops.cross_entropy_bwd(logits, target, row_lse, g), None
+
+
+def cross_entropy(logits, target):
+    """F.cross_entropy(logits, target) (mean), fused softmax-CE fwd/bwd kernels."""
+    L.require_gpu(logits)
+    return _CrossEntropyFn.apply(logits, target)
+
+
+# ----------------------------------------------------------------------------
+# modules (timm key layout)
+# ----------------------------------------------------------------------------
+
+class PatchEmbed(nn.Module):
+    def __init__(self, img_size, patch_size, in_chans, embed_dim):
+        super().__init__()
+        self.img_size, self.patch_size = img_size, patch_size
+        self.num_patches = (img_size // patch_size) ** 2
+        self.proj = nn.Conv2d(in_chans, embed_dim, patch_size, patch_size)
+
+
+class Attention(nn.Module):
+    def __init__(self, dim, num_heads):
+        super().__init__()
+        self.num_heads = num_heads
+        self.head_dim = dim // num_heads
+        self.scale = self.head_dim ** -0.5
+        self.qkv = nn.Linear(dim, 3 * dim)
+        self.proj = nn.Linear(dim, dim)
+
+
+class Mlp(nn.Module):
+    def __init__(self, dim, hidden):
+        super().__init__()
+        self.fc1 = nn.Linear(dim, hidden)
+        self.fc2 = nn.Linear(hidden, dim)
+
+
+class Block(nn.Module):
+    def __init__(self, dim, num_heads, mlp_ratio, eps):
+        super().__init__()
+        self.norm1 = nn.LayerNorm(dim, eps=eps)
+        self.attn = Attention(dim, num_heads)
+        self.norm2 = nn.LayerNorm(dim, eps=eps)
+        self.mlp = Mlp(dim, int(dim * mlp_ratio))
+
+    def block_params(self):
+        return (self.norm1.weight, self.norm1.bias, self.attn.qkv.weight, self.attn.qkv.bias,
+                self.attn.proj.weight, self.attn.proj.bias, self.norm2.weight, self.norm2.bias,
+                self.mlp.fc1.weight, self.mlp.fc1.bias, self.mlp.fc2.weight, self.mlp.fc2.bias)
+
+
+class VisionTransformer(nn.Module):
+    """timm ``VisionTransformer`` (class-token, pre-norm, global_pool='token')."""
+
+    def __init__(self, img_size=224, patch_size=16, in_chans=3, num_classes=1000, embed_dim=768, depth=12,
+                 num_heads=12, mlp_ratio=4.0, eps=1e-6, quick_gelu=False, compute_dtype=torch.bfloat16):
+        super().__init__()
+        if embed_dim // num_heads != 64:
+            raise ValueError("the HIP attention kernels require head_dim 64")
+        self.num_classes = num_classes
+        self.embed_dim = self.num_features = embed_dim
+        self.global_pool = "token"
+        self.num_prefix_tokens = 1
+        self.compute_dtype = compute_dtype
+        self._cfg = dict(heads=num_heads, eps=eps, quick_gelu=quick_gelu, dtype=compute_dtype, patch=patch_size)
+        self.cls_token = nn.Parameter(torch.zeros(1, 1, embed_dim))
+        self.patch_embed = PatchEmbed(img_size, patch_size, in_chans, embed_dim)
+        self.pos_embed = nn.Parameter(torch.zeros(1, self.patch_embed.num_patches + 1, embed_dim))
+        self.blocks = nn.Sequential(*[Block(embed_dim, num_heads, mlp_ratio, eps) for _ in range(depth)])
+        self.norm = nn.LayerNorm(embed_dim, eps=eps)
+        self.head = nn.Linear(embed_dim, num_classes)
+        self._shadows = None
+        self.init_weights()
+
+    # timm init_weights_vit_timm; exact RNG stream differs from timm
+    @torch.no_grad()
+    def init_weights(self, seed=None):
+        g = torch.Generator().manual_seed(seed) if seed is not None else None
+        nn.init.trunc_normal_(self.pos_embed, std=0.02, generator=g)
+        nn.init.normal_(self.cls_token, std=1e-6, generator=g)
+        for m in self.modules():
+            if isinstance(m, nn.Linear):
+                nn.init.trunc_normal_(m.weight, std=0.02, generator=g)
+                nn.init.zeros_(m.bias)
+
+    def load_oracle_params(self, params: "OrderedDict[str, torch.Tensor]"):
+        """Copy a timm-keyed fp32 state dict (e.g. the oracle's) into this model."""
+        self.load_state_dict(params, strict=True)
+
+    # -- device / dtype plumbing --------------------------------------------------
+    def _ensure_shadows(self):
+        dev = self.cls_token.device
+        if self._shadows is None or self._shadows_device != dev:
+            self._shadows = _Shadowed()
+            self._shadows_device = dev
+            ws = [self.patch_embed.proj.weight]
+            for blk in self.blocks:
+                ws += [blk.attn.qkv.weight, blk.attn.proj.weight, blk.mlp.fc1.weight, blk.mlp.fc2.weight]
+            for p in ws:
+                self._shadows.add(p, self.compute_dtype)
+        self._shadows.refresh()
+
+    def use_flat_grads(self, enable: bool = True):
+        """Write every gradient into one flat fp32 buffer (backward order: head
+        first, patch embed last) -- ``flat_grad`` is what a data-parallel
+        all-reduce reduces (vit_amd.parallel)."""
+        params = list(self.parameters())
+        if not enable:
+            for p in params:
+                p._vit_flat_grad = None
+            self.flat_grad = None
+            return None
+        order = [self.norm.weight, self.norm.bias, self.head.weight, self.head.bias]
+        for blk in reversed(list(self.blocks)):
+            order += list(reversed(blk.block_params()))
+        pe = self.patch_embed.proj
+        order += [pe.weight, pe.bias, self.cls_token, self.pos_embed]
+        assert len(order) == len(params) and {id(p) for p in order} == {id(p) for p in params}
+        n = sum(p.numel() for p in order)
+        flat = torch.zeros(n, dtype=torch.float32, device=self.cls_token.device)
+        off = 0
+        self.flat_grad_slices = []
+        for p in order:
+            p._vit_flat_grad = flat[off:off + p.numel()].view(p.shape)
+            self.flat_grad_slices.append((off, p.numel()))
+            off += p.numel()
+        self.flat_grad = flat
+        return flat
+
+    def shadow_params(self):
+        self._ensure_shadows()
+        return list(self._shadows.pairs)
+
+    # -- timm surface ----------------------------------------------------------------
+    def _tokens(self, x):
+        L.require_gpu(x)
+        self._ensure_shadows()
+        cfg = dict(self._cfg)
+        pe = self.patch_embed
+        x = _PatchEmbedFn.apply(x.to(torch.float32), pe.proj.weight, pe.proj.bias, self.cls_token, self.pos_embed,
+                                cfg)
+        n = len(self.blocks)
+        for i, blk in enumerate(self.blocks):
+            bcfg = cfg if i != 0 else dict(cfg, compact_np=pe.num_patches)
+            x = _BlockFn.apply(x, *blk.block_params(), bcfg)
+        return x
+
+    def forward_features(self, x):
+        """post-norm tokens [B, N, D] (f32), as timm forward_features (MEAS:309)."""
+        x = self._tokens(x)
+        B, N, D = x.shape
+        # full final norm (inference / RSA path; forward() only normalises CLS rows)
+        y, _, _ = ops.layer_norm_fwd(x.reshape(B * N, D), self.norm.weight.detach(), self.norm.bias.detach(),
+                                     self._cfg["eps"], torch.float32, need_stats=False)
+        return y.reshape(B, N, D)
+
+    def forward_head(self, feats, pre_logits=False):
+        x = feats[:, 0]
+        return x if pre_logits else ops.linear_fwd(x.contiguous(), self.head.weight.detach(),
+                                                   self.head.bias.detach(), out_dtype=torch.float32)
+
+    def forward(self, x):
+        x = self._tokens(x)
+        return _HeadFn.apply(x, self.norm.weight, self.norm.bias, self.head.weight, self.head.bias, dict(self._cfg))
+
+
+_MODEL_CFGS = {
+    "vit_base_patch16_224": dict(img_size=224, patch_size=16, embed_dim=768, depth=12, num_heads=12),
+    "vit_large_patch16_224": dict(img_size=224, patch_size=16, embed_dim=1024, depth=24, num_heads=16),
+    "vit_small_patch16_224": dict(img_size=224, patch_size=16, embed_dim=384, depth=12, num_heads=6),
+}
+
+
+def create_model(name: str, pretrained: bool = False, num_classes: int = 1000, compute_dtype=torch.bfloat16,
+                 **kw):
+    """``timm.create_model`` drop-in for the configs the reference uses (VIT:283)."""
+    if pretrained:
+        raise ValueError("pretrained weights are not available offline")
+    if name not in _MODEL_CFGS:
+        raise KeyError(f"unknown model {name}; known: {sorted(_MODEL_CFGS)}")
+    cfg = dict(_MODEL_CFGS[name])
+    cfg.update(kw)
+    return VisionTransformer(num_classes=num_classes, compute_dtype=compute_dtype, **cfg)

@@ -1,0 +1,225 @@
+"""Tensor-level wrappers over the C-ABI kernels (no compute happens in Python).
+
+Every function takes torch tensors that live on the ROCm device, launches the
+HIP kernel on the current stream and returns.  These mirror the torch ops the
+reference's hot path reaches through timm:
+
+  linear_fwd / linear_dgrad / linear_wgrad   F.linear fwd / bwd  (timm Attention.qkv/proj, Mlp.fc1/fc2, head)
+  layer_norm_fwd / layer_norm_bwd            F.layer_norm         (timm Block.norm1/norm2, final norm)
+  sdpa_fwd / sdpa_bwd                        F.scaled_dot_product_attention
+  patch_unfold + patch_embed_fwd             Conv2d(k16, s16) + cat(cls) + pos_embed (timm PatchEmbed/_pos_embed)
+  cross_entropy_fwd / _bwd                   F.cross_entropy (VIT:140)
+  sgd_step                                   torch.optim.SGD.step (VIT:294-299)
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from ._lib import call, ptr
+
+_WS = {}
+
+
+def workspace(name: str, nbytes: int, device) -> torch.Tensor:
+    """Grow-only scratch buffer, reused across calls on the same stream."""
+    key = (name, torch.device(device))
+    t = _WS.get(key)
+    if t is None or t.numel() < nbytes:
+        t = torch.empty(max(nbytes, 256), dtype=torch.uint8, device=device)
+        _WS[key] = t
+    return t
+
+
+def _s(t: torch.Tensor) -> int:
+    return L.stream_ptr(t.device)
+
+
+# ----------------------------------------------------------------------------
+# GEMMs
+# ----------------------------------------------------------------------------
+
+def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, resid=None, act_out=None):
+    """y = epi(x @ w^T + bias).  x2d [M,K] (row stride x2d.stride(0)), w [N,K] contiguous."""
+    L.require_gpu(x2d)
+    M, K = x2d.shape
+    N = w.shape[0]
+    assert w.shape[1] == K and w.is_contiguous() and x2d.stride(1) == 1
+    assert w.dtype == x2d.dtype
+    if out is None:
+        if epi == L.EPI_RESID:
+            od = torch.float32
+        else:
+            od = out_dtype or x2d.dtype
+        out = torch.empty(M, N, dtype=od, device=x2d.device)
+    if epi in (L.EPI_BIAS_GELU, L.EPI_BIAS_QGELU):
+        if act_out is None:
+            act_out = torch.empty_like(out)
+    if epi == L.EPI_RESID:
+        assert resid is not None and resid.dtype == torch.float32 and out.dtype == torch.float32
+        assert resid.stride(0) == out.stride(0)
+    call("vit_linear_fwd", L.dt(x2d), L.dt(out), epi, M, N, K, ptr(x2d), x2d.stride(0), ptr(w), ptr(bias),
+         ptr(out), out.stride(0), ptr(resid), ptr(act_out), _s(x2d))
+    return (out, act_out) if epi in (L.EPI_BIAS_GELU, L.EPI_BIAS_QGELU) else out
+
+
+def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, out=None):
+    """dx = dy @ w  (dy [M,N], w [N,K]) with optional activation-grad epilogue on pre [M,K]."""
+    M, N = dy2d.shape
+    K = w.shape[1]
+    assert w.shape[0] == N and w.dtype == dy2d.dtype and dy2d.stride(1) == 1
+    if out is None:
+        out = torch.empty(M, K, dtype=out_dtype, device=dy2d.device)
+    if pre is not None:
+        assert pre.stride(0) == out.stride(0)
+    call("vit_linear_dgrad", L.dt(dy2d), L.dt(out), epi, M, N, K, ptr(dy2d), dy2d.stride(0), ptr(w), ptr(out),
+         out.stride(0), ptr(pre), _s(dy2d))
+    return out
+
+
+def _wgrad_split(M, N, K):
+    # enough workgroups to cover the 256 CUs several times; chunks of >= 512 rows
+    tiles = max(1, (N // 128) * (K // 128))
+    want = max(1, min(32, (1024 + tiles - 1) // tiles))
+    return max(1, min(want, M // 512))
+
+
+def linear_wgrad(dy2d, x2d, out=None, split=None):
+    """dW [N,K] (f32) = dy^T @ x,  dy [M,N], x [M,K]."""
+    M, N = dy2d.shape
+    K = x2d.shape[1]
+    assert x2d.shape[0] == M and x2d.dtype == dy2d.dtype
+    if out is None:
+        out = torch.empty(N, K, dtype=torch.float32, device=dy2d.device)
+    if split is None:
+        split = _wgrad_split(M, N, K)
+    ws = workspace("wgrad", split * N * K * 4, dy2d.device) if split > 1 else None
+    call("vit_linear_wgrad", L.dt(dy2d), M, N, K, ptr(dy2d), dy2d.stride(0), ptr(x2d), x2d.stride(0), ptr(out),
+         split, ptr(ws), 0 if ws is None else ws.numel(), _s(dy2d))
+    return out
+
+
+def colsum(x2d, out=None, accumulate=False):
+    """out[N] (f32) = x.sum(0)."""
+    M, N = x2d.shape
+    if out is None:
+        out = torch.empty(N, dtype=torch.float32, device=x2d.device)
+    S = max(1, min(256, M // 64))
+    part = workspace("colsum", S * N * 4, x2d.device)
+    call("vit_colsum", L.dt(x2d), M, N, ptr(x2d), x2d.stride(0), ptr(out), ptr(part), S * N, int(accumulate),
+         _s(x2d))
+    return out
+
+
+# ----------------------------------------------------------------------------
+# LayerNorm
+# ----------------------------------------------------------------------------
+
+def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, need_stats=True):
+    rows = x2d.shape[0] if rows is None else rows
+    D = w.numel()
+    ldx = x2d.stride(0) if ldx is None else ldx
+    if out is None:
+        out = torch.empty(rows, D, dtype=out_dtype, device=x2d.device)
+    mean = rstd = None
+    if need_stats:
+        mean = torch.empty(rows, dtype=torch.float32, device=x2d.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=x2d.device)
+    call("vit_layer_norm_fwd", L.dt(x2d), L.dt(out), rows, D, ptr(x2d), ldx, ptr(out), out.stride(0), ptr(w),
+         ptr(b), ptr(mean), ptr(rstd), float(eps), _s(x2d))
+    return out, mean, rstd
+
+
+def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0, dx_copy=None, ld_copy=0,
+                   compact_np=0, dgamma=None, dbeta=None):
+    D = w.numel()
+    part = None
+    nfl = 0
+    if dgamma is not None:
+        nblk = (rows + 63) // 64
+        nfl = 2 * nblk * D
+        part = workspace("ln_partial", nfl * 4, x.device)
+    call("vit_layer_norm_bwd", L.dt(x), L.dt(dy), rows, D, ptr(x), ldx, ptr(dy), dy.stride(0), ptr(w), ptr(mean),
+         ptr(rstd), ptr(dres), ldres, ptr(dx), lddx, ptr(dx_copy), ld_copy,
+         L.dt(dx_copy) if dx_copy is not None else L.BF16, compact_np, ptr(dgamma), ptr(dbeta), ptr(part), nfl,
+         _s(x))
+
+
+# ----------------------------------------------------------------------------
+# attention
+# ----------------------------------------------------------------------------
+
+def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None):
+    D = H * 64
+    if o is None:
+        o = torch.empty(B * N, D, dtype=qkv2d.dtype, device=qkv2d.device)
+    lse = torch.empty(B * H * N, dtype=torch.float32, device=qkv2d.device)
+    scale = 64 ** -0.5 if scale is None else scale
+    call("vit_sdpa_fwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(lse),
+         float(scale), _s(qkv2d))
+    return o, lse
+
+
+def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None):
+    if dqkv is None:
+        dqkv = torch.empty_like(qkv2d)
+    scale = 64 ** -0.5 if scale is None else scale
+    delta = workspace("sdpa_delta", B * H * N * 4, qkv2d.device)
+    call("vit_sdpa_bwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(do),
+         do.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), ptr(delta), float(scale), _s(qkv2d))
+    return dqkv
+
+
+# ----------------------------------------------------------------------------
+# patch embed, CE, casts
+# ----------------------------------------------------------------------------
+
+def patch_unfold(img, ps, dtype):
+    B, C, Hi, Wi = img.shape
+    assert img.dtype == torch.float32 and img.is_contiguous()
+    npatch = (Hi // ps) * (Wi // ps)
+    U = torch.empty(B * npatch, C * ps * ps, dtype=dtype, device=img.device)
+    call("vit_patch_unfold", L.dt(U), B, C, Hi, Wi, ps, ptr(img), ptr(U), _s(img))
+    return U
+
+
+def patch_embed_fwd(U, w2d, bias, pos, cls, B, npatch):
+    D, K = w2d.shape
+    x = torch.empty(B, npatch + 1, D, dtype=torch.float32, device=U.device)
+    call("vit_patch_embed_fwd", L.dt(U), B, npatch, D, K, ptr(U), ptr(w2d), ptr(bias), ptr(pos), ptr(x), _s(U))
+    call("vit_cls_pos_fill", B, npatch + 1, D, ptr(x), ptr(cls), ptr(pos), _s(U))
+    return x
+
+
+def pos_grad(dx, B, S, D, dpos, dcls):
+    call("vit_pos_grad", B, S, D, ptr(dx), ptr(dpos), ptr(dcls), _s(dx))
+
+
+def cross_entropy_fwd(logits, target):
+    B, C = logits.shape
+    assert logits.dtype == torch.float32 and target.dtype == torch.int64
+    row_lse = torch.empty(B, dtype=torch.float32, device=logits.device)
+    row_loss = torch.empty(B, dtype=torch.float32, device=logits.device)
+    loss = torch.empty((), dtype=torch.float32, device=logits.device)
+    call("vit_cross_entropy_fwd", B, C, ptr(logits), logits.stride(0), ptr(target), ptr(row_lse), ptr(row_loss),
+         ptr(loss), _s(logits))
+    return loss, row_lse
+
+
+def cross_entropy_bwd(logits, target, row_lse, grad_loss, out_dtype=torch.float32):
+    B, C = logits.shape
+    d = torch.empty(B, C, dtype=out_dtype, device=logits.device)
+    g = grad_loss.to(torch.float32).contiguous() if grad_loss is not None else None
+    call("vit_cross_entropy_bwd", L.dt(d), B, C, ptr(logits), logits.stride(0), ptr(target), ptr(row_lse), ptr(g),
+         ptr(d), d.stride(0), _s(logits))
+    return d
+
+
+def cast_bf16(src: torch.Tensor, dst: torch.Tensor):
+    assert src.dtype == torch.float32 and dst.dtype == torch.bfloat16 and src.numel() == dst.numel()
+    call("vit_cast_f32_bf16", ptr(src), ptr(dst), src.numel(), _s(src))
+
+
+def zero_(t: torch.Tensor):
+    call("vit_zero", ptr(t), t.numel() * t.element_size(), _s(t))
+    return t

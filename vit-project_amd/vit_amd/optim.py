@@ -1,0 +1,223 @@
+"""Fused optimizers and the reference LR schedule.
+
+``FusedSGD`` is ``torch.optim.SGD(params, lr, momentum, weight_decay)`` (VIT:294-299,
+dampening 0, nesterov off) as ONE multi-tensor HIP launch over every parameter:
+``d = g + wd*p; buf = momentum*buf + d; p -= lr*buf`` (zero-initialised ``buf``
+makes the first step identical to torch's ``buf = d.clone()``), writing the bf16
+GEMM shadow of each weight in the same pass.  ``lr`` lives in a device scalar so
+a captured HIP graph follows the schedule (call :meth:`sync_lr` outside the graph).
+
+``FusedAdamW`` is ``torch.optim.AdamW`` (NEWP:1181; amsgrad off) the same way.
+``CosineAnnealingLRWithWarmup`` restates VIT:206-244 (stepped once per epoch
+after training, so epoch 0 runs at the base LR: quirk Q1).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from ._lib import call
+
+
+def _table(entries, struct_fields):
+    """Pack a list of tuples into a device table matching the C struct layout
+    {ptr, ptr, ptr, ptr, int64} (5 x 8 bytes)."""
+    arr = np.zeros((len(entries), struct_fields), dtype=np.int64)
+    for i, e in enumerate(entries):
+        arr[i] = [0 if v is None else int(v) for v in e]
+    return arr
+
+
+class _MultiTensor:
+    CHUNK = 4096
+
+    def __init__(self, device):
+        self.device = device
+        self._key = None
+        self._tdev = None
+        self._cdev = None
+        self._pinned = None
+        self.nchunks = 0
+
+    def build(self, entries, sizes):
+        key = tuple(tuple(0 if v is None else int(v) for v in e) for e in entries)
+        if key == self._key:
+            return
+        t = _table(entries, 5)
+        chunks = []
+        for i, n in enumerate(sizes):
+            for s in range(0, n, self.CHUNK):
+                chunks.append((i, s))
+        c = np.zeros((len(chunks), 2), dtype=np.int64)
+        for k, (i, s) in enumerate(chunks):
+            c[k, 0] = i  # {int tensor; int pad} packed little-endian in one int64
+            c[k, 1] = s
+        tb = torch.from_numpy(t.reshape(-1).view(np.uint8).copy())
+        cb = torch.from_numpy(c.reshape(-1).view(np.uint8).copy())
+        host = torch.cat([tb, cb]).pin_memory() if torch.cuda.is_available() else torch.cat([tb, cb])
+        dev = torch.empty(host.numel(), dtype=torch.uint8, device=self.device)
+        dev.copy_(host, non_blocking=True)
+        self._pinned = host  # keep alive for async copy / graph replay
+        self._tdev = dev[: tb.numel()]
+        self._cdev = dev[tb.numel():]
+        self.nchunks = len(chunks)
+        self._key = key
+
+
+class FusedSGD(torch.optim.Optimizer):
+    def __init__(self, params, lr=0.1, momentum=0.9, weight_decay=1e-4, dampening=0.0, nesterov=False):
+        if dampening != 0 or nesterov:
+            raise ValueError("FusedSGD implements the reference configuration: dampening 0, nesterov False")
+        super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, dampening=0.0,
+                                      nesterov=False))
+        self._mt = None
+        self._lr_dev = None
+        self._lr_host = None
+
+    def _device(self):
+        for g in self.param_groups:
+            for p in g["params"]:
+                return p.device
+        return None
+
+    def sync_lr(self):
+        """Copy param_groups[0]['lr'] into the device scalar the kernel reads."""
+        lrs = {g["lr"] for g in self.param_groups}
+        if len(lrs) != 1:
+            raise ValueError("FusedSGD supports one LR across param groups")
+        lr = lrs.pop()
+        dev = self._device()
+        if self._lr_dev is None:
+            self._lr_dev = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+            self._lr_host = lr
+        elif lr != self._lr_host:
+            self._lr_dev.fill_(float(lr))
+            self._lr_host = lr
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        dev = self._device()
+        L.require_gpu(torch.empty(0, device=dev))
+        if self._mt is None:
+            self._mt = _MultiTensor(dev)
+        if self._lr_dev is None or not torch.cuda.is_current_stream_capturing():
+            self.sync_lr()
+        g0 = self.param_groups[0]
+        mom, wd = g0["momentum"], g0["weight_decay"]
+        for g in self.param_groups:
+            if g["momentum"] != mom or g["weight_decay"] != wd:
+                raise ValueError("FusedSGD supports one (momentum, weight_decay) across groups")
+        entries, sizes = [], []
+        for g in self.param_groups:
+            for p in g["params"]:
+                if p.grad is None:
+                    continue
+                if p.grad.dtype != torch.float32 or not p.grad.is_contiguous():
+                    p.grad = p.grad.float().contiguous()
+                st = self.state[p]
+                if "momentum_buffer" not in st:
+                    st["momentum_buffer"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                sh = getattr(p, "_vit_shadow", None)
+                entries.append((p.data_ptr(), p.grad.data_ptr(), st["momentum_buffer"].data_ptr(),
+                                None if sh is None else sh.data_ptr(), p.numel()))
+                sizes.append(p.numel())
+        if not entries:
+            return loss
+        self._mt.build(entries, sizes)
+        call("vit_sgd_step", self._mt._tdev.data_ptr(), self._mt._cdev.data_ptr(), self._mt.nchunks,
+             self._lr_dev.data_ptr(), float(mom), float(wd), L.stream_ptr(dev))
+        # shadows are now in sync with the (raw-pointer) update; mark them fresh
+        for g in self.param_groups:
+            for p in g["params"]:
+                if getattr(p, "_vit_shadow", None) is not None and p.grad is not None:
+                    p._vit_shadow_version = p._version
+        return loss
+
+
+class FusedAdamW(torch.optim.Optimizer):
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
+        self._mt = None
+        self._lr_dev = None
+        self._step_dev = None
+        self._nstep = 0
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        g0 = self.param_groups[0]
+        dev = g0["params"][0].device
+        L.require_gpu(torch.empty(0, device=dev))
+        if self._mt is None:
+            self._mt = _MultiTensor(dev)
+            self._lr_dev = torch.empty(1, dtype=torch.float32, device=dev)
+            self._step_dev = torch.empty(1, dtype=torch.float32, device=dev)
+        self._nstep += 1
+        self._lr_dev.fill_(float(g0["lr"]))
+        self._step_dev.fill_(float(self._nstep))
+        entries, sizes = [], []
+        for p in g0["params"]:
+            if p.grad is None:
+                continue
+            st = self.state[p]
+            if "exp_avg" not in st:
+                st["exp_avg"] = torch.zeros_like(p)
+                st["exp_avg_sq"] = torch.zeros_like(p)
+                st["step"] = torch.zeros((), dtype=torch.float32)
+            st["step"] += 1
+            entries.append((p.data_ptr(), p.grad.contiguous().data_ptr(), st["exp_avg"].data_ptr(),
+                            st["exp_avg_sq"].data_ptr(), p.numel()))
+            sizes.append(p.numel())
+        if not entries:
+            return loss
+        self._mt.build(entries, sizes)
+        b1, b2 = g0["betas"]
+        call("vit_adamw_step", self._mt._tdev.data_ptr(), self._mt._cdev.data_ptr(), self._mt.nchunks,
+             self._lr_dev.data_ptr(), self._step_dev.data_ptr(), float(b1), float(b2), float(g0["eps"]),
+             float(g0["weight_decay"]), L.stream_ptr(dev))
+        return loss
+
+
+class CosineAnnealingLRWithWarmup:
+    """Linear warmup then cosine, stepped once per epoch (VIT:206-244)."""
+
+    def __init__(self, optimizer, warmup_epochs, max_epochs, eta_min=0):
+        self.optimizer = optimizer
+        self.warmup_epochs = warmup_epochs
+        self.max_epochs = max_epochs
+        self.eta_min = eta_min
+        self.base_lrs = [g["lr"] for g in optimizer.param_groups]
+        self.current_epoch = 0
+
+    def lr_at(self, c: int, base_lr: float) -> float:
+        if c < self.warmup_epochs:
+            return base_lr * ((c + 1) / self.warmup_epochs)
+        progress = (c - self.warmup_epochs) / (self.max_epochs - self.warmup_epochs)
+        return self.eta_min + (base_lr - self.eta_min) * 0.5 * (1 + math.cos(math.pi * progress))
+
+    def step(self):
+        for g, base in zip(self.optimizer.param_groups, self.base_lrs):
+            g["lr"] = self.lr_at(self.current_epoch, base)
+        self.current_epoch += 1
+
+    def state_dict(self):
+        return {"current_epoch": self.current_epoch, "base_lrs": self.base_lrs,
+                "warmup_epochs": self.warmup_epochs, "max_epochs": self.max_epochs, "eta_min": self.eta_min}
+
+    def load_state_dict(self, sd):
+        self.current_epoch = sd["current_epoch"]
+        self.base_lrs = sd["base_lrs"]
+        self.warmup_epochs = sd["warmup_epochs"]
+        self.max_epochs = sd["max_epochs"]
+        self.eta_min = sd["eta_min"]
