@@ -103,6 +103,8 @@ def main():
             loss = step()
     torch.cuda.current_stream(dev).wait_stream(s)
     torch.cuda.synchronize(dev)
+    warm_loss = float(loss.item())
+    del loss
     graph = None
     if use_graph:
         graph = torch.cuda.CUDAGraph()
@@ -131,7 +133,7 @@ def main():
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    final_loss = float((gloss if graph is not None else loss).item())
+    final_loss = float(gloss.item()) if graph is not None else warm_loss
 
     # --- dominant-kernel roofline: fc1 forward GEMM (M=B*197, N=3072, K=768, bias+GELU epilogue),
     #     timed with HIP events on the stream it is launched on

@@ -44,6 +44,9 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
              const void* P, int64_t ldp, const void* Q, int64_t ldq, void* C, int64_t ldc,
              const float* bias, const void* aux, int64_t ld_aux, void* aux_out, int allow_fast, void* stream);
 
+/* Tuning hook: force GEMM tile configuration v (see csrc/gemm.hip big::V*), -1 = per-shape choice. */
+int vit_gemm_variant(int v);
+
 /* F.linear forward, Y = X W^T + b with fused epilogue (timm Attention.qkv/proj,
  * Mlp.fc1+GELU / fc2 + residual, head; under VIT:138-139 autocast). */
 int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const void* X, int64_t ldx,

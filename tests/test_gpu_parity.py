@@ -69,6 +69,9 @@ def test_tiny_f32_full_step_matches_golden(golden_dir):
     p = R.init_params(cfg, seed=fx["seed"], random_affine=True)
     x, y = _inputs(cfg, fx["B"], fx["seed"])
     m = _model(cfg, p, torch.float32)
+    with torch.no_grad():
+        f = m.forward_features(x.to(DEV))
+    assert _rel(f, fx["features"]) < 1e-3
     logits, loss, grads = _step(m, x, y)
     assert _rel(logits, fx["logits"]) < 1e-3
     assert abs(loss.item() - fx["loss"]) < 1e-3 * abs(fx["loss"])
@@ -76,8 +79,14 @@ def test_tiny_f32_full_step_matches_golden(golden_dir):
         assert _rel(g, fx["grads"][k]) < 1e-3, k
     for k, v in m.state_dict().items():
         assert _rel(v, fx["params_after"][k]) < 1e-3, k
-    f = m.forward_features(x.to(DEV))
-    assert _rel(f, fx["features"]) < 1e-3
+    # flat-gradient mode (the data-parallel / bench configuration) gives the same step
+    m2 = _model(cfg, p, torch.float32)
+    m2.use_flat_grads(True)
+    _, _, grads2 = _step(m2, x, y)
+    for k, g in grads2.items():
+        assert _rel(g, grads[k]) < 1e-6, k
+    for (k, a), (_, b) in zip(m.state_dict().items(), m2.state_dict().items()):
+        assert _rel(b, a) < 1e-6, k
 
 
 def test_vit_b16_f32_step_matches_golden(golden_dir):
@@ -149,6 +158,7 @@ def test_bf16_batch32_matches_oracle_and_graph_replay():
     with torch.no_grad():
         ref = R.forward(p, x[:4], cfg)
     m = _model(cfg, p, torch.bfloat16)
+    m.use_flat_grads(True)
     opt = vit_amd.FusedSGD(m.parameters(), lr=0.05)
     xd, yd = x.to(DEV), y.to(DEV)
     with torch.no_grad():
@@ -156,6 +166,7 @@ def test_bf16_batch32_matches_oracle_and_graph_replay():
     assert _rel(logits[:4], ref) < 3e-2
     # second model: same weights, graph-captured steps
     m2 = _model(cfg, p, torch.bfloat16)
+    m2.use_flat_grads(True)  # fixed gradient addresses: the optimizer table is built once, outside capture
     opt2 = vit_amd.FusedSGD(m2.parameters(), lr=0.05)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
@@ -166,6 +177,7 @@ def test_bf16_batch32_matches_oracle_and_graph_replay():
             opt2.step()
             opt2.zero_grad(set_to_none=True)
     torch.cuda.current_stream().wait_stream(s)
+    del l2
     # the warmup took one step on m2: the eager model takes its first here
     logits = m(xd)
     loss = vit_amd.cross_entropy(logits, yd)

@@ -33,17 +33,42 @@ __device__ __forceinline__ bf16x8 at_tr_frag(const char* img, int row0, int d0, 
   return cat4(lo, hi);
 }
 
-// Load rows [0, N) of a head's 64-wide slice into an LDS image of `rows` rows,
-// zero-filling rows >= N.
-__device__ __forceinline__ void at_load(char* img, const bf16* src, int64_t ld, int N, int rows) {
-  for (int idx = threadIdx.x; idx < rows * 8; idx += blockDim.x) {
-    int row = idx >> 3, c = idx & 7;
-    bf16x8 v;
-    if (row < N) v = *reinterpret_cast<const bf16x8*>(src + (int64_t)row * ld + c * 8);
-    else { for (int t = 0; t < 8; ++t) v[t] = (bf16)0.f; }
-    *reinterpret_cast<bf16x8*>(img + at_off(row, c)) = v;
-  }
+// Load rows [0, N) of NM head slices (64 wide) into LDS images of ROWS rows,
+// zero-filling rows >= N.  All global loads of the thread are issued before the
+// first LDS write (one latency, not one per chunk); rows >= N load a clamped
+// valid row and are zeroed in registers.
+template <int ROWS, int NTHR, int NM>
+__device__ __forceinline__ void at_load(char* const (&img)[NM], const bf16* const (&src)[NM],
+                                        const int64_t (&ld)[NM], int N) {
+  constexpr int TOTAL = ROWS * 8, PER = (TOTAL + NTHR - 1) / NTHR;
+  bf16x8 v[NM][PER];
+#pragma unroll
+  for (int mtx = 0; mtx < NM; ++mtx)
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = threadIdx.x + u * NTHR;
+      const int row = min(idx >> 3, N - 1), c = idx & 7;
+      if (idx < TOTAL) v[mtx][u] = *reinterpret_cast<const bf16x8*>(src[mtx] + (int64_t)row * ld[mtx] + c * 8);
+    }
+#pragma unroll
+  for (int mtx = 0; mtx < NM; ++mtx)
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = threadIdx.x + u * NTHR;
+      const int row = idx >> 3, c = idx & 7;
+      if (idx < TOTAL) {
+        bf16x8 w = v[mtx][u];
+        if (row >= N) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) w[t] = (bf16)0.f;
+        }
+        *reinterpret_cast<bf16x8*>(img[mtx] + at_off(row, c)) = w;
+      }
+    }
 }
+
+constexpr int AT_THREADS = 512;  // 8 waves per (batch, head)
+constexpr int AT_WAVES = AT_THREADS / 64;
 
 __device__ __forceinline__ bf16x8 pack8(const f32x4& a, const f32x4& b) {
   return bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
@@ -56,7 +81,7 @@ constexpr float LN2 = 0.6931471805599453f;
 // bf16 forward
 // ---------------------------------------------------------------------------
 template <int NT>  // key/query tiles of 16: NT = ceil(N/16)
-__global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D,
+__global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D,
                                                      int H, int N, float scale, bf16* __restrict__ o,
                                                      int64_t ld_o, float* __restrict__ lse) {
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
@@ -66,11 +91,15 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16* __restrict__ qk
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const bf16* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
-  at_load(Kimg, base + D, ld_qkv, N, ROWS);
-  at_load(Vimg, base + 2 * D, ld_qkv, N, ROWS);
+  {
+    char* const imgs[2] = {Kimg, Vimg};
+    const bf16* const srcs[2] = {base + D, base + 2 * D};
+    const int64_t lds_[2] = {ld_qkv, ld_qkv};
+    at_load<ROWS, AT_THREADS, 2>(imgs, srcs, lds_, N);
+  }
   __syncthreads();
   const float c2 = scale * LOG2E;
-  for (int qt = wave; qt < NT; qt += 4) {
+  for (int qt = wave; qt < NT; qt += AT_WAVES) {
     const int q = qt * 16 + (lane & 15);
     bf16x8 qf[2];
 #pragma unroll
@@ -84,6 +113,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16* __restrict__ qk
       s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) s[kt] = mfma16(at_row_frag(Kimg, kt * 16, kk, lane), qf[kk], s[kt]);
+      if (kt % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound K-fragment hoisting (VGPRs)
     }
     float m = -INFINITY;
 #pragma unroll
@@ -113,6 +143,7 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16* __restrict__ qk
       bf16x8 pf = pack8(s[2 * ks], hi);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma16(at_tr_frag(Vimg, ks * 32, dt * 16, lane), pf, oacc[dt]);
+      if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // bound V-fragment hoisting (VGPRs)
     }
     if (q < N) {
       const float inv = 1.0f / l;
@@ -132,11 +163,11 @@ __global__ __launch_bounds__(256) void attn_fwd_mfma(const bf16* __restrict__ qk
 // bf16 backward: phase 1 key-parallel (dK, dV), phase 2 query-parallel (dQ).
 // ---------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(256) void attn_bwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+__global__ __launch_bounds__(AT_THREADS) void attn_bwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H,
                                                      int N, float scale, const bf16* __restrict__ o, int64_t ld_o,
                                                      const bf16* __restrict__ dout, int64_t ld_do,
-                                                     const float* __restrict__ lse, bf16* __restrict__ dqkv,
-                                                     int64_t ld_dqkv) {
+                                                     const float* __restrict__ lse, const float* __restrict__ delta_in,
+                                                     bf16* __restrict__ dqkv, int64_t ld_dqkv) {
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Qimg = smem;
@@ -149,27 +180,28 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const bf16* __restrict__ qk
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
   const bf16* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
   const bf16* dob = dout + (int64_t)b * N * ld_do + h * 64;
-  at_load(Qimg, base, ld_qkv, N, ROWS);
-  at_load(Kimg, base + D, ld_qkv, N, ROWS);
-  at_load(Vimg, base + 2 * D, ld_qkv, N, ROWS);
-  at_load(Oimg, dob, ld_do, N, ROWS);
-  // delta[q] = sum_d dO*O (one wave per row, 64 lanes = 64 dims), lse in log2 units
-  for (int q = wave; q < ROWS; q += 4) {
-    float dsum = 0.f;
-    if (q < N) {
-      dsum = (float)dob[(int64_t)q * ld_do + lane] * (float)o[((int64_t)b * N + q) * ld_o + h * 64 + lane];
-      dsum = wave_sum(dsum);
-    }
-    if (lane == 0) {
-      delta[q] = dsum;
-      lse2[q] = (q < N) ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
-    }
+  {
+    char* const imgs[2] = {Qimg, Kimg};
+    const bf16* const srcs[2] = {base, base + D};
+    const int64_t lds_[2] = {ld_qkv, ld_qkv};
+    at_load<ROWS, AT_THREADS, 2>(imgs, srcs, lds_, N);
+  }
+  {
+    char* const imgs[2] = {Vimg, Oimg};
+    const bf16* const srcs[2] = {base + 2 * D, dob};
+    const int64_t lds_[2] = {ld_qkv, ld_do};
+    at_load<ROWS, AT_THREADS, 2>(imgs, srcs, lds_, N);
+  }
+  // per-query constants: delta[q] = sum_d dO*O (precomputed, attn_delta_kernel), lse in log2 units
+  for (int q = threadIdx.x; q < ROWS; q += AT_THREADS) {
+    delta[q] = (q < N) ? delta_in[(int64_t)bh * N + q] : 0.f;
+    lse2[q] = (q < N) ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
   }
   __syncthreads();
   const float c2 = scale * LOG2E;
 
   // ---- phase 1: key tiles -> dK, dV
-  for (int kt = wave; kt < NT; kt += 4) {
+  for (int kt = wave; kt < NT; kt += AT_WAVES) {
     const int key = kt * 16 + (lane & 15);
     bf16x8 kf[2], vf[2];
 #pragma unroll
@@ -180,6 +212,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const bf16* __restrict__ qk
     f32x4 dv[4], dk[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) { dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[dt] = dv[dt]; }
+#pragma unroll 1
     for (int qp = 0; qp < NT2; ++qp) {
       f32x4 p[2], ds[2];
 #pragma unroll
@@ -220,7 +253,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const bf16* __restrict__ qk
   }
 
   // ---- phase 2: query tiles -> dQ
-  for (int qt = wave; qt < NT; qt += 4) {
+  for (int qt = wave; qt < NT; qt += AT_WAVES) {
     const int q = qt * 16 + (lane & 15);
     bf16x8 qf[2], of[2];
 #pragma unroll
@@ -232,6 +265,7 @@ __global__ __launch_bounds__(256) void attn_bwd_mfma(const bf16* __restrict__ qk
     f32x4 dq[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
     for (int kp = 0; kp < NT2; ++kp) {
       f32x4 ds[2];
 #pragma unroll
@@ -420,19 +454,47 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_generic(const T* __restrict_
   for (int d = 0; d < 16; ++d) { row[D + d] = (T)(dk[d] * scale); row[2 * D + d] = (T)dv[d]; }
 }
 
+// delta[(b*H + h)*N + n] = sum_d dO[b*N+n][h*64+d] * O[b*N+n][h*64+d]; 16 lanes
+// per (row, head), 4 dims per lane (8-B loads), shuffle-reduced.
+template <typename T>
+__global__ __launch_bounds__(256) void attn_delta_kernel(const T* __restrict__ o, int64_t ld_o,
+                                                         const T* __restrict__ dout, int64_t ld_do, int B, int H,
+                                                         int N, float* __restrict__ delta) {
+  const int64_t pair = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);
+  const int l = threadIdx.x & 15;
+  const bool ok = pair < (int64_t)B * N * H;
+  float s = 0.f;
+  int64_t row = 0;
+  int h = 0;
+  if (ok) {
+    row = pair / H;
+    h = (int)(pair - row * H);
+    const T* op = o + row * ld_o + h * 64 + l * 4;
+    const T* dp = dout + row * ld_do + h * 64 + l * 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) s = fmaf((float)op[t], (float)dp[t], s);
+  }
+#pragma unroll
+  for (int m = 8; m > 0; m >>= 1) s += __shfl_xor(s, m, 64);
+  if (ok && l == 0) {
+    const int b = (int)(row / N), n = (int)(row - (int64_t)b * N);
+    delta[((int64_t)b * H + h) * N + n] = s;
+  }
+}
+
 // ---------------------------------------------------------------------------
 template <int NT>
 static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, void* o,
                     int64_t ld_o, float* lse, hipStream_t s) {
-  hipLaunchKernelGGL((attn_fwd_mfma<NT>), dim3(B * H), dim3(256), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
+  hipLaunchKernelGGL((attn_fwd_mfma<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
                      (bf16*)o, ld_o, lse);
   VIT_CHECK_LAUNCH();
   return 0;
 }
 template <int NT>
 static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, const void* o,
-                    int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
-                    hipStream_t s) {
+                    int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const float* delta,
+                    void* dqkv, int64_t ld_dqkv, hipStream_t s) {
   constexpr int ROWS = ((NT + 1) / 2) * 32;
   size_t lds = 4 * ROWS * 128 + 2 * ROWS * sizeof(float);
   static bool attr_set = false;
@@ -440,8 +502,8 @@ static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N,
     (void)hipFuncSetAttribute((const void*)attn_bwd_mfma<NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set = true;
   }
-  hipLaunchKernelGGL((attn_bwd_mfma<NT>), dim3(B * H), dim3(256), lds, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
-                     (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, (bf16*)dqkv, ld_dqkv);
+  hipLaunchKernelGGL((attn_bwd_mfma<NT>), dim3(B * H), dim3(AT_THREADS), lds, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
+                     (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, delta, (bf16*)dqkv, ld_dqkv);
   VIT_CHECK_LAUNCH();
   return 0;
 }
@@ -476,22 +538,26 @@ int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
 }
 
 // SDPA backward: writes dq/dk/dv into dqkv (same column layout as qkv).
-// `delta_ws` (>= B*H*N floats) is scratch for the generic path (may be null on the bf16 path).
+// `delta_ws` (>= B*H*N floats) receives rowsum(dO*O) per (b, h, n).
 int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, const void* o,
                  int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
                  float* delta_ws, float scale, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (head_dim != 64 || N <= 0 || N > 288) return (int)hipErrorInvalidValue;
   const int D = H * 64;
-  if (dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_do % 8 == 0) && (ld_dqkv % 4 == 0)) {
+  if (!delta_ws) return (int)hipErrorInvalidValue;
+  if (dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_do % 8 == 0) && (ld_dqkv % 4 == 0) && (ld_o % 4 == 0)) {
+    const int64_t pairs = (int64_t)B * N * H;
+    hipLaunchKernelGGL(attn_delta_kernel<bf16>, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, s, (const bf16*)o,
+                       ld_o, (const bf16*)dout, ld_do, B, H, N, delta_ws);
+    VIT_CHECK_LAUNCH();
     int nt = (N + 15) / 16;
     switch (nt) {
-#define CASE(n) case n: return bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, dout, ld_do, lse, dqkv, ld_dqkv, s);
+#define CASE(n) case n: return bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, s);
       NT_CASES(CASE)
 #undef CASE
     }
   }
-  if (!delta_ws) return (int)hipErrorInvalidValue;
   dim3 grid((N + 63) / 64, B * H);
 #define GEN(T)                                                                                               \
   hipLaunchKernelGGL(attn_bwd_dq_generic<T>, grid, dim3(256), 0, s, (const T*)qkv, ld_qkv, D, H, N, scale,    \

@@ -18,11 +18,12 @@
 // Generic path (any shape/stride, f32 or bf16 in, fp32 FMA): parity mode and
 // odd shapes (classifier head N=1000).
 #include "common.hpp"
+#include "reduce.hpp"
 #include <string.h>
 
 enum { LAY_RC = 0, LAY_CR = 1 };
 enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_PATCH = 4,
-       EPI_BIAS_QGELU = 5, EPI_QGELU_BWD = 6 };
+       EPI_BIAS_QGELU = 5, EPI_QGELU_BWD = 6, EPI_ACC = 7 };
 
 struct Epi {
   void* C; int64_t ldc;
@@ -53,21 +54,25 @@ template <> __device__ __forceinline__ f32x4 load4<bf16>(const bf16* p) {
 
 // Apply the epilogue to 4 consecutive output columns j..j+3 of row i.
 template <int EPI, typename TO, typename TA>
-__device__ __forceinline__ void epi4(const Epi& e, int i, int j, f32x4 v) {
+__device__ __forceinline__ void epi4(const Epi& e, int i, int j, f32x4 v, int z = 0) {
   if (e.bias) {
     f32x4 b = *reinterpret_cast<const f32x4*>(e.bias + j);
     v += b;
   }
   if constexpr (EPI == EPI_STORE) {
-    store4<TO>((TO*)e.C + e.slab * blockIdx.z + (int64_t)i * e.ldc + j, v);
+    store4<TO>((TO*)e.C + e.slab * z + (int64_t)i * e.ldc + j, v);
+  } else if constexpr (EPI == EPI_ACC) {
+    TO* c = (TO*)e.C + (int64_t)i * e.ldc + j;
+    store4<TO>(c, v + load4<TO>(c));
   } else if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) {
-    f32x4 pre_r;
     // the activation is computed from the rounded pre-activation that backward sees
     store4<TO>((TO*)e.C + (int64_t)i * e.ldc + j, v);
-    pre_r = load4<TO>((const TO*)e.C + (int64_t)i * e.ldc + j);
+    f32x4 pre_r;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) pre_r[t] = (float)(TO)v[t];
     f32x4 a;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) a[t] = (EPI == EPI_BIAS_GELU) ? gelu_erf(pre_r[t]) : quick_gelu(pre_r[t]);
+    for (int t = 0; t < 4; ++t) a[t] = (EPI == EPI_BIAS_GELU) ? gelu_fast(pre_r[t]) : quick_gelu(pre_r[t]);
     store4<TO>((TO*)e.aux_out + (int64_t)i * e.ldc + j, a);
   } else if constexpr (EPI == EPI_RESID) {
     f32x4 r = load4<float>((const float*)e.aux + (int64_t)i * e.ld_aux + j);
@@ -75,7 +80,7 @@ __device__ __forceinline__ void epi4(const Epi& e, int i, int j, f32x4 v) {
   } else if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
     f32x4 pre = load4<TA>((const TA*)e.aux + (int64_t)i * e.ld_aux + j);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] *= (EPI == EPI_GELU_BWD) ? gelu_erf_grad(pre[t]) : quick_gelu_grad(pre[t]);
+    for (int t = 0; t < 4; ++t) v[t] *= (EPI == EPI_GELU_BWD) ? gelu_fast_grad(pre[t]) : quick_gelu_grad(pre[t]);
     store4<TO>((TO*)e.C + (int64_t)i * e.ldc + j, v);
   } else if constexpr (EPI == EPI_PATCH) {
     int b = i / e.n_patch, p = i - b * e.n_patch;
@@ -91,6 +96,9 @@ __device__ __forceinline__ void epi1(const Epi& e, int i, int j, float v) {
   if (e.bias) v += e.bias[j];
   if constexpr (EPI == EPI_STORE) {
     ((TO*)e.C)[e.slab * blockIdx.z + (int64_t)i * e.ldc + j] = (TO)v;
+  } else if constexpr (EPI == EPI_ACC) {
+    TO* c = (TO*)e.C + (int64_t)i * e.ldc + j;
+    *c = (TO)((float)*c + v);
   } else if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) {
     TO pr = (TO)v;
     ((TO*)e.C)[(int64_t)i * e.ldc + j] = pr;
@@ -110,131 +118,222 @@ __device__ __forceinline__ void epi1(const Epi& e, int i, int j, float v) {
 }
 
 // ----------------------------------------------------------------------------
-// Fast bf16 kernel
+// Fast bf16 kernel, parametrised: BM x BN x BK tile, WI x WJ waves (each a
+// (BM/WI) x (BN/WJ) wave tile of 16x16 accumulators), an S-deep LDS ring filled
+// by global_load_lds with a counted vmcnt (S-2 k-steps stay in flight across the
+// single s_barrier per k-step), optional register double-buffering of the MFMA
+// fragments (DB: the next k-step's ds_reads overlap this k-step's MFMAs), OCC =
+// minimum waves per SIMD (sets the VGPR budget / workgroups per CU).
 // ----------------------------------------------------------------------------
-namespace fast {
-constexpr int BM = 128, BN = 128, BK = 64;
-constexpr int IMG = 128 * 64 * 2;       // bytes of one operand image (16 KiB)
-constexpr int STAGE = 2 * IMG;           // P + Q
-constexpr int LDS_BYTES = 2 * STAGE;     // double buffer: 64 KiB
+namespace big {
 
-// r-contiguous image: 128 rows x 64 r (128 B rows); chunk c (16 B) of row at
-// row*128 + ((c ^ ((row>>1)&7)) << 4).  Conflict-free for the 16x16x32 fragment
-// ds_read_b128 pattern (16 consecutive rows, chunks g+4kk).
-__device__ __forceinline__ int rc_off(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
-// r-strided image: 64 r-rows x 128 cols (256 B rows); chunk c in 0..15 at
-// r*256 + ((c ^ f(r)) << 4), f(r) = ((r&3)<<2)|((r>>2)&3).  Conflict-free for the
-// two ds_read_b64_tr_b16 of a 16x16x32 fragment (rows 8g+q and 8g+4+q).
+template <int BM_, int BN_, int BK_, int WI_, int WJ_, int S_, bool DB_, int OCC_> struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WI = WI_, WJ = WJ_, STAGES = S_, OCC = OCC_;
+  static constexpr bool DB = DB_;
+  static constexpr int WAVES = WI * WJ, THREADS = WAVES * 64;
+  static constexpr int WM = BM / WI, WN = BN / WJ;
+  static constexpr int AI = WM / 16, AJ = WN / 16, KS = BK / 32;
+  static constexpr int PIMG = BM * BK * 2, QIMG = BN * BK * 2;
+  static constexpr int STAGE = PIMG + QIMG;
+  static constexpr int GP = PIMG / 1024 / WAVES, GQ = QIMG / 1024 / WAVES;
+  static constexpr int G = GP + GQ;  // global_load_lds per wave per stage
+  static constexpr int LDS = STAGES * STAGE;
+  static_assert(GP * 1024 * WAVES == PIMG && GQ * 1024 * WAVES == QIMG, "stage must split into 1-KiB pieces per wave");
+  static_assert(LDS <= 163840, "LDS");
+};
+
+// r-contiguous image, BK=32: 64-B rows, chunk c at row*64 + ((c ^ h(row)) << 4),
+// h(row) = (row & 1) | ((row >> 1) & 2).  BK=64: 128-B rows, chunk c at
+// row*128 + ((c ^ ((row >> 1) & 7)) << 4).  Both conflict-free for the 16x16x32
+// ds_read_b128 fragment pattern (tools/lds_banks.py).
+template <int BK> __device__ __forceinline__ int rc_sw(int row) {
+  if constexpr (BK == 32) return (row & 1) | ((row >> 1) & 2);
+  else return (row >> 1) & 7;
+}
+template <int BK> __device__ __forceinline__ int rc_off(int row, int c) {
+  return row * (BK * 2) + ((c ^ rc_sw<BK>(row)) << 4);
+}
+// r-strided image: BK r-rows x COLS (COLS*2-byte rows), chunk c at
+// r*COLS*2 + (((c & ~15) | ((c & 15) ^ f(r))) << 4), f(r) = ((r&3)<<2)|((r>>2)&3):
+// conflict-free for the two ds_read_b64_tr_b16 of a fragment (rows 8g+q, 8g+4+q).
 __device__ __forceinline__ int cr_f(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
-__device__ __forceinline__ int cr_off(int r, int c) { return r * 256 + ((c ^ cr_f(r)) << 4); }
+__device__ __forceinline__ int cr_swz(int c, int r) { return (c & ~15) | ((c & 15) ^ cr_f(r)); }
+template <int COLS> __device__ __forceinline__ int cr_off(int r, int c) { return r * COLS * 2 + (cr_swz(c, r) << 4); }
 
-// Stage one 128x64 operand tile into an LDS image with global_load_lds.
-// RC: 16 wave-instructions of 8 rows; CR: 16 of 4 r-rows.  Each wave issues 4.
-template <int LAY>
-__device__ __forceinline__ void stage(char* img, const bf16* base, int64_t ld, int row0, int r0, int wave, int lane) {
+// Stage a ROWS x BK operand tile into an LDS image; each wave issues G_OP 1-KiB
+// global_load_lds.  Rows (RC) / columns (CR) past `lim` are clamped to valid
+// memory; their outputs are never stored.
+template <int LAY, int ROWS, int BK, int G_OP>
+__device__ __forceinline__ void stage(char* img, const bf16* __restrict__ base, int64_t ld, int row0, int r0,
+                                      int lim, int wave, int lane) {
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    int t = wave * 4 + u;
+  for (int u = 0; u < G_OP; ++u) {
+    const int t = wave * G_OP + u;
     const bf16* src;
     if constexpr (LAY == LAY_RC) {
-      int row = t * 8 + (lane >> 3);
-      int c = (lane & 7) ^ ((row >> 1) & 7);
-      src = base + (int64_t)(row0 + row) * ld + r0 + c * 8;
+      constexpr int CPR = BK / 8, RPI = 64 / CPR;
+      const int row = t * RPI + lane / CPR;
+      const int c = (lane % CPR) ^ rc_sw<BK>(row);
+      const int grow = min(row0 + row, lim - 1);
+      src = base + (int64_t)grow * ld + r0 + c * 8;
     } else {
-      int r = t * 4 + (lane >> 4);
-      int c = (lane & 15) ^ cr_f(r);
-      src = base + (int64_t)(r0 + r) * ld + row0 + c * 8;
+      constexpr int CPR = ROWS / 8;  // 16-B chunks per r-row
+      constexpr int RPI = 64 / CPR;  // r-rows per wave-instruction
+      const int r = t * RPI + lane / CPR;
+      const int c = cr_swz(lane % CPR, r);
+      const int col = min(row0 + c * 8, lim - 8);
+      src = base + (int64_t)(r0 + r) * ld + col;
     }
     __builtin_amdgcn_global_load_lds((const void*)src, LDS_PTR(img + t * 1024), 16, 0, 0);
   }
 }
 
-// Fragment for rows s*16..s*16+15 of the tile, r-substep kk (32 wide).
-template <int LAY>
+// fragment of rows s*16..s*16+15, k-substep kk (16x16x32 operand, natural k order)
+template <int LAY, int ROWS, int BK>
 __device__ __forceinline__ bf16x8 frag(const char* img, int s, int kk, int lane) {
   if constexpr (LAY == LAY_RC) {
-    int row = s * 16 + (lane & 15);
-    int c = kk * 4 + (lane >> 4);
-    return *reinterpret_cast<const bf16x8*>(img + rc_off(row, c));
+    return *reinterpret_cast<const bf16x8*>(img + rc_off<BK>(s * 16 + (lane & 15), kk * 4 + (lane >> 4)));
   } else {
-    int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    int c = 2 * s + (p >> 1);
-    int r0 = kk * 32 + 8 * g + q;
-    int r1 = r0 + 4;
-    bf16x4 lo = lds_read_tr(img + cr_off(r0, c) + (p & 1) * 8);
-    bf16x4 hi = lds_read_tr(img + cr_off(r1, c) + (p & 1) * 8);
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int c = 2 * s + (p >> 1);
+    const int r0 = kk * 32 + 8 * g + q;
+    bf16x4 lo = lds_read_tr(img + cr_off<ROWS>(r0, c) + (p & 1) * 8);
+    bf16x4 hi = lds_read_tr(img + cr_off<ROWS>(r0 + 4, c) + (p & 1) * 8);
     return cat4(lo, hi);
   }
 }
 
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  // bijective: blocks that share an XCD (bid % 8) get a contiguous range of tiles
+  // bijective: blocks that share an XCD (bid % 8) get a contiguous range of ids
   int xcd = bid & 7, q = nwg >> 3, r = nwg & 7, k = bid >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
 }
 
-template <int PL, int QL, int EPI, typename TO, typename TA>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(const bf16* __restrict__ P, int64_t ldp,
-                                                      const bf16* __restrict__ Q, int64_t ldq,
-                                                      int M, int N, int R, int r_chunk, Epi e) {
-  __shared__ __attribute__((aligned(16))) char smem[LDS_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tiles_j = N / BN;
-  const int nwg = gridDim.x;
-  const int t = xcd_remap(blockIdx.x, nwg);
+template <int N> __device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// wait until at most n stages (of G loads each) of this wave remain in flight
+template <int G, int S>
+__device__ __forceinline__ void wait_stages(int n) {
+  if constexpr (S >= 6) { if (n >= 5) { wait_vm<5 * G>(); return; } }
+  if constexpr (S >= 5) { if (n >= 4) { wait_vm<4 * G>(); return; } }
+  if constexpr (S >= 4) { if (n >= 3) { wait_vm<3 * G>(); return; } }
+  if constexpr (S >= 3) { if (n >= 2) { wait_vm<2 * G>(); return; } }
+  if (n >= 1) { wait_vm<G>(); return; }
+  wait_vm<0>();
+}
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <class C, int PL, int QL, int EPI, typename TO, typename TA>
+__global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __restrict__ P, int64_t ldp,
+                                                                  const bf16* __restrict__ Q, int64_t ldq,
+                                                                  int M, int N, int R, int r_chunk, Epi e) {
+  constexpr int S = C::STAGES, BM = C::BM, BN = C::BN, BK = C::BK;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // 1-D grid over (split, tile): consecutive ids share an XCD after the remap,
+  // so a split's workgroups (same rows of P and Q) sit on one L2
+  const int tiles_j = (N + BN - 1) / BN;
+  const int tiles = ((M + BM - 1) / BM) * tiles_j;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = w / tiles, t = w - z * tiles;
   const int ti = t / tiles_j, tj = t - ti * tiles_j;
   const int i0 = ti * BM, j0 = tj * BN;
-  const int rb = blockIdx.z * r_chunk;
+  const int rb = z * r_chunk;
   const int re = min(R, rb + r_chunk);
   const int nk = (re - rb) / BK;
-  const int wi = wave >> 1, wj = wave & 1;
+  const int wi = wave / C::WJ, wj = wave % C::WJ;
 
-  f32x4 acc[4][4];
+  f32x4 acc[C::AI][C::AJ];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < C::AI; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < C::AJ; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issue = [&](int k) {
+    char* buf = smem + (k % S) * C::STAGE;
+    stage<PL, BM, BK, C::GP>(buf, P, ldp, i0, rb + k * BK, M, wave, lane);
+    stage<QL, BN, BK, C::GQ>(buf + C::PIMG, Q, ldq, j0, rb + k * BK, N, wave, lane);
+  };
+  auto load_frags = [&](int k, int kk, bf16x8 (&pf)[C::AI], bf16x8 (&qf)[C::AJ]) {
+    const char* cur = smem + (k % S) * C::STAGE;
+#pragma unroll
+    for (int b = 0; b < C::AJ; ++b) qf[b] = frag<QL, BN, BK>(cur + C::PIMG, wj * C::AJ + b, kk, lane);
+#pragma unroll
+    for (int a = 0; a < C::AI; ++a) pf[a] = frag<PL, BM, BK>(cur, wi * C::AI + a, kk, lane);
+  };
+  auto mma = [&](const bf16x8 (&pf)[C::AI], const bf16x8 (&qf)[C::AJ]) {
+#pragma unroll
+    for (int a = 0; a < C::AI; ++a)
+#pragma unroll
+      for (int b = 0; b < C::AJ; ++b) acc[a][b] = mfma16(qf[b], pf[a], acc[a][b]);
+  };
 
   if (nk > 0) {
-    stage<PL>(smem, P, ldp, i0, rb, wave, lane);
-    stage<QL>(smem + IMG, Q, ldq, j0, rb, wave, lane);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = smem + (kt & 1) * STAGE;
-    if (kt + 1 < nk) {
-      char* nxt = smem + ((kt + 1) & 1) * STAGE;
-      stage<PL>(nxt, P, ldp, i0, rb + (kt + 1) * BK, wave, lane);
-      stage<QL>(nxt + IMG, Q, ldq, j0, rb + (kt + 1) * BK, wave, lane);
+#pragma unroll
+    for (int k = 0; k < S - 1; ++k)
+      if (k < nk) issue(k);
+    if constexpr (!C::DB) {
+      for (int kt = 0; kt < nk; ++kt) {
+        wait_stages<C::G, S>(min(S - 2, nk - 1 - kt));
+        lds_barrier();
+        if (kt + S - 1 < nk) issue(kt + S - 1);
+#pragma unroll
+        for (int kk = 0; kk < C::KS; ++kk) {
+          bf16x8 pf[C::AI], qf[C::AJ];
+          load_frags(kt, kk, pf, qf);
+          mma(pf, qf);
+        }
+      }
+    } else {
+      static_assert(C::KS == 1, "register double-buffering is built for BK = 32");
+      // step k: make stage k+1 readable, refill slot k%S with stage k+S-1... (ring of S, S-1 ahead)
+      auto step = [&](int k, const bf16x8 (&pc)[C::AI], const bf16x8 (&qc)[C::AJ], bf16x8 (&pn)[C::AI],
+                      bf16x8 (&qn)[C::AJ]) {
+        if (k + 1 < nk) {
+          wait_stages<C::G, S>(min(S - 3, nk - 2 - k));
+          lds_barrier();
+          if (k + S - 1 < nk) issue(k + S - 1);
+          load_frags(k + 1, 0, pn, qn);
+        }
+        mma(pc, qc);
+      };
+      bf16x8 pA[C::AI], qA[C::AJ], pB[C::AI], qB[C::AJ];
+      wait_stages<C::G, S>(min(S - 2, nk - 1));
+      lds_barrier();
+      load_frags(0, 0, pA, qA);
+      int kt = 0;
+      for (; kt + 1 < nk; kt += 2) {
+        step(kt, pA, qA, pB, qB);
+        step(kt + 1, pB, qB, pA, qA);
+      }
+      if (kt < nk) step(kt, pA, qA, pB, qB);
     }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 pf[4], qf[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) pf[a] = frag<PL>(cur, wi * 4 + a, kk, lane);
-#pragma unroll
-      for (int b = 0; b < 4; ++b) qf[b] = frag<QL>(cur + IMG, wj * 4 + b, kk, lane);
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = mfma16(qf[b], pf[a], acc[a][b]);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
   // epilogue: acc[a][b] holds C[i][j..j+3] with i = lane&15, j = 4*(lane>>4)
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    int i = i0 + wi * 64 + a * 16 + (lane & 15);
+  for (int a = 0; a < C::AI; ++a) {
+    const int i = i0 + wi * C::WM + a * 16 + (lane & 15);
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      int j = j0 + wj * 64 + b * 16 + 4 * (lane >> 4);
-      epi4<EPI, TO, TA>(e, i, j, acc[a][b]);
+    for (int b = 0; b < C::AJ; ++b) {
+      const int j = j0 + wj * C::WN + b * 16 + 4 * (lane >> 4);
+      if (i < M && j < N) epi4<EPI, TO, TA>(e, i, j, acc[a][b], z);
     }
   }
 }
-}  // namespace fast
+
+// the configurations kept after the sweep (tools/bench_kernels.py --sweep; DESIGN.md
+// lists the measured TFLOP/s per shape).  Others tried: 256x256x32 S5 with register
+// double-buffering (1 WG/CU; wgrad 360-400 TF), 128x128x32 S4, 256x128x64 S3, 128x256x32 S4.
+//            BM   BN  BK WI WJ  S  DB    OCC
+using V1 = Cfg<256, 128, 32, 4, 2, 3, false, 4>;  //  72 KiB, 2 WG/CU: dgrad
+using V2 = Cfg<128, 128, 64, 2, 2, 2, false, 2>;  //  64 KiB, 2 WG/CU (4 waves): N = 768 forward
+using V5 = Cfg<256, 256, 64, 2, 4, 2, false, 2>;  // 128 KiB, 1 WG/CU: wide forward, wgrad
+}  // namespace big
 
 // ----------------------------------------------------------------------------
 // Generic strided kernel: any M, N, R; f32 or bf16 inputs; fp32 FMA.
@@ -331,36 +430,66 @@ __global__ void colsum_partial_kernel(const T* __restrict__ X, int64_t ld, int M
   part[(int64_t)blockIdx.y * N + j] = (s0 + s1) + (s2 + s3);
 }
 
-__global__ void colsum_final_kernel(const float* __restrict__ part, int S, int N, float* __restrict__ out,
-                                    int accumulate) {
-  int j = blockIdx.x * 256 + threadIdx.x;
-  if (j >= N) return;
-  float s = 0.f;
-  for (int z = 0; z < S; ++z) s += part[(int64_t)z * N + j];
-  out[j] = accumulate ? out[j] + s : s;
-}
 
 // ----------------------------------------------------------------------------
 // host dispatch
 // ----------------------------------------------------------------------------
+// fast-path eligibility: bf16, 16-B aligned operands, 8-element row strides,
+// reduction length a multiple of BK (callers split off a ragged tail).
 static bool fast_ok(int dtype, int M, int N, int R, const void* P, const void* Q, int64_t ldp, int64_t ldq) {
   if (dtype != VIT_BF16) return false;
-  if (M % fast::BM || N % fast::BN || R % fast::BK) return false;
+  if (M % 8 || N % 8 || R % 32 || R <= 0) return false;
   if ((ldp % 8) || (ldq % 8)) return false;
   if (((uintptr_t)P & 15) || ((uintptr_t)Q & 15)) return false;
   return true;
 }
 
-template <int PL, int QL, int EPI, typename TO, typename TA>
-static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R,
-                       int split, const Epi& e, hipStream_t s) {
-  int r_chunk = ((R / split + fast::BK - 1) / fast::BK) * fast::BK;
-  int nz = (R + r_chunk - 1) / r_chunk;
-  dim3 grid((M / fast::BM) * (N / fast::BN), 1, nz);
-  hipLaunchKernelGGL((fast::gemm_kernel<PL, QL, EPI, TO, TA>), grid, dim3(256), 0, s,
+static int g_variant = -1;  // -1: per-shape choice; 1, 2, 5: force big::V<n> (tuning)
+
+// per-shape choice among the kept configurations (sweep on MI355X, bs=256 ViT-B/16 shapes)
+static int pick_variant(int pl, int ql, int M, int N, int R, int split) {
+  int v;
+  if (g_variant >= 0) v = g_variant;
+  else if (split > 1 || (pl == LAY_CR && ql == LAY_CR)) v = 5;  // wgrad: 256x256 tiles, split-K sized for them
+  else if (pl == LAY_RC && ql == LAY_RC) v = N >= 1536 ? 5 : 2;
+  else v = 1;                                                   // dgrad (r-strided Q)
+  (void)M;
+  if (v != 1 && R % 64) v = 1;                                  // BK = 64 configurations need 64-row chunks
+  return v;
+}
+
+static int r_chunk_for(int R, int split, int bk) {
+  int c = ((R / split + bk - 1) / bk) * bk;
+  return c > 0 ? c : bk;
+}
+
+template <class C, int PL, int QL, int EPI, typename TO, typename TA>
+static int launch_big(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
+                      const Epi& e, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)big::gemm_kernel<C, PL, QL, EPI, TO, TA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  if (R % C::BK) return (int)hipErrorInvalidValue;
+  const int r_chunk = r_chunk_for(R, split, 64);  // one chunking for every variant (wgrad counts slabs)
+  const int nz = (R + r_chunk - 1) / r_chunk;
+  dim3 grid(((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN) * nz);
+  hipLaunchKernelGGL((big::gemm_kernel<C, PL, QL, EPI, TO, TA>), grid, dim3(C::THREADS), C::LDS, s,
                      (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, r_chunk, e);
   VIT_CHECK_LAUNCH();
   return 0;
+}
+
+template <int PL, int QL, int EPI, typename TO, typename TA>
+static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R,
+                       int split, const Epi& e, hipStream_t s) {
+  switch (pick_variant(PL, QL, M, N, R, split)) {
+    case 2: return launch_big<big::V2, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    case 5: return launch_big<big::V5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    default: return launch_big<big::V1, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+  }
 }
 
 template <typename T, int EPI, typename TO, typename TA>
@@ -414,6 +543,7 @@ static int gemm_any(int epi, int dtype, int out_dtype, int pl, int ql, int M, in
     case EPI_RESID: return gemm_dispatch<EPI_RESID>(dtype, out_dtype, pl, ql, M, N, R, P, ldp, Q, ldq, split, e, s, allow_fast);
     case EPI_GELU_BWD: return gemm_dispatch<EPI_GELU_BWD>(dtype, out_dtype, pl, ql, M, N, R, P, ldp, Q, ldq, split, e, s, allow_fast);
     case EPI_QGELU_BWD: return gemm_dispatch<EPI_QGELU_BWD>(dtype, out_dtype, pl, ql, M, N, R, P, ldp, Q, ldq, split, e, s, allow_fast);
+    case EPI_ACC: return gemm_dispatch<EPI_ACC>(dtype, out_dtype, pl, ql, M, N, R, P, ldp, Q, ldq, split, e, s, allow_fast);
     case EPI_PATCH: return gemm_dispatch<EPI_PATCH>(dtype, out_dtype, pl, ql, M, N, R, P, ldp, Q, ldq, split, e, s, allow_fast);
   }
   return (int)hipErrorInvalidValue;
@@ -422,6 +552,9 @@ static int gemm_any(int epi, int dtype, int out_dtype, int pl, int ql, int M, in
 static Epi make_epi() { Epi e; memset(&e, 0, sizeof(e)); return e; }
 
 extern "C" {
+
+// Tuning hook: force GEMM configuration big::V<v> (-1 restores the per-shape heuristic).
+int vit_gemm_variant(int v) { g_variant = v; return 0; }
 
 // Raw dispatcher (exported for tests/benchmarks of individual layouts).
 int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int M, int N, int R,
@@ -459,25 +592,34 @@ int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t ldd
                      int64_t ldx, float* dW, int split, void* workspace, int64_t ws_bytes, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (split < 1) split = 1;
+  if (M <= 0) return (int)hipMemsetAsync(dW, 0, (size_t)N * K * 4, s);
+  // the MFMA kernel takes the BK-aligned rows; a ragged tail (M % 32) is added by the generic kernel
+  const int tail = M % 32;
+  const bool fast = (M - tail) > 0 && fast_ok(dtype, N, K, M - tail, dY, X, lddy, ldx);
+  const int R0 = fast ? M - tail : M;
   if (split > 1 && (workspace == nullptr || ws_bytes < (int64_t)split * N * K * 4)) return (int)hipErrorInvalidValue;
   Epi e = make_epi();
+  int rc;
   if (split == 1) {
     e.C = dW; e.ldc = K;
-    return gemm_any(EPI_STORE, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, M, dY, lddy, X, ldx, 1, e, s);
+    rc = gemm_any(EPI_STORE, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, R0, dY, lddy, X, ldx, 1, e, s, fast);
+  } else {
+    e.C = workspace; e.ldc = K; e.slab = (int64_t)N * K;
+    const int r_chunk = r_chunk_for(R0, split, fast ? 64 : gen::TK);
+    const int nz = (R0 + r_chunk - 1) / r_chunk;
+    rc = gemm_any(EPI_STORE, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, R0, dY, lddy, X, ldx, split, e, s, fast);
+    if (rc) return rc;
+    const int64_t n = (int64_t)N * K;
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0, s,
+                       (const float*)workspace, nz, n, dW);
+    VIT_CHECK_LAUNCH();
   }
-  e.C = workspace; e.ldc = K; e.slab = (int64_t)N * K;
-  // the launchers round the chunk to the tile depth; count the real slabs
-  bool fast = fast_ok(dtype, N, K, M, dY, X, lddy, ldx);
-  int tk = fast ? fast::BK : gen::TK;
-  int r_chunk = ((M / split + tk - 1) / tk) * tk;
-  int nz = (M + r_chunk - 1) / r_chunk;
-  int rc = gemm_any(EPI_STORE, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, M, dY, lddy, X, ldx, split, e, s);
-  if (rc) return rc;
-  int64_t n = (int64_t)N * K;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n / 4 + 255) / 256 + 1)), dim3(256), 0, s,
-                     (const float*)workspace, nz, n, dW);
-  VIT_CHECK_LAUNCH();
-  return 0;
+  if (rc || R0 == M) return rc;
+  Epi t = make_epi();
+  t.C = dW; t.ldc = K;
+  const size_t esz = dtype == VIT_BF16 ? 2 : 4;
+  return gemm_any(EPI_ACC, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, M - R0, (const char*)dY + (size_t)R0 * lddy * esz,
+                  lddy, (const char*)X + (size_t)R0 * ldx * esz, ldx, 1, t, s, false);
 }
 
 // Column sum (bias grads): out[N] (f32) = sum_i X[i*ld + j]; partial buffer >= S*N floats
@@ -498,7 +640,7 @@ int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, f
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, M, N, rows_per, partial);
   VIT_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, partial, S, N, out, accumulate);
+  launch_colreduce(partial, S, N, out, accumulate, s);
   VIT_CHECK_LAUNCH();
   return 0;
 }

@@ -8,6 +8,7 @@
 // NV = float4 groups per lane (D = 256*NV: 3 for ViT-B's 768, 4 for 1024); a
 // scalar kernel (NV = 0) covers any other D (test configs).
 #include "common.hpp"
+#include "reduce.hpp"
 
 constexpr int LN_WAVES = 4;   // rows per block in the forward (one per wave)
 constexpr int LN_SMAX = 32;   // scalar path: D <= 64*32
@@ -171,13 +172,6 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
   }
 }
 
-__global__ void partial_reduce_kernel(const float* __restrict__ part, int S, int D, float* __restrict__ out) {
-  int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= D) return;
-  float s = 0.f;
-  for (int z = 0; z < S; ++z) s += part[(int64_t)z * D + c];
-  out[c] = s;
-}
 
 template <typename TX, typename TY>
 static void launch_fwd(int nv, dim3 grid, hipStream_t s, const void* x, int64_t ldx, void* y, int64_t ldy,
@@ -266,9 +260,9 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
 #undef LB
   VIT_CHECK_LAUNCH();
   if (dgamma) {
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((D + 255) / 256), dim3(256), 0, s, pg, nblk, D, dgamma);
+    launch_colreduce(pg, nblk, D, dgamma, 0, s);
     VIT_CHECK_LAUNCH();
-    hipLaunchKernelGGL(partial_reduce_kernel, dim3((D + 255) / 256), dim3(256), 0, s, pb, nblk, D, dbeta);
+    launch_colreduce(pb, nblk, D, dbeta, 0, s);
     VIT_CHECK_LAUNCH();
   }
   return 0;

@@ -84,7 +84,7 @@ def _gout(p: nn.Parameter) -> torch.Tensor:
     fresh tensor, so autograd's accumulation stays correct)."""
     fb = getattr(p, "_vit_flat_grad", None)
     if fb is not None and (p.grad is None or p.grad.data_ptr() != fb.data_ptr()):
-        return fb
+        return fb.view(fb.shape)  # a fresh alias AccumulateGrad can steal (no copy)
     return torch.empty(p.shape, dtype=torch.float32, device=p.device)
 
 
@@ -173,7 +173,7 @@ class _BlockFn(torch.autograd.Function):
         dpre = ops.linear_dgrad(dxo_c, _w(fc2w), out_dtype=T, epi=gelu_bwd, pre=pre)
         d_fc2w = ops.linear_wgrad(dxo_c, act, out=_gout(fc2w))
         d_fc2b = ops.colsum(dxo_c, out=_gout(fc2b))
-        dh2 = ops.linear_dgrad(dpre, _w(fc1w), out_dtype=torch.float32)
+        dh2 = ops.linear_dgrad(dpre, _w(fc1w), out_dtype=T)
         d_fc1w = ops.linear_wgrad(dpre, h2, out=_gout(fc1w))
         d_fc1b = ops.colsum(dpre, out=_gout(fc1b))
         dxm = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
@@ -186,7 +186,7 @@ class _BlockFn(torch.autograd.Function):
         d_projw = ops.linear_wgrad(dxm_c, o, out=_gout(projw))
         d_projb = ops.colsum(dxm_c, out=_gout(projb))
         dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N)
-        dh1 = ops.linear_dgrad(dqkv, _w(qkvw), out_dtype=torch.float32)
+        dh1 = ops.linear_dgrad(dqkv, _w(qkvw), out_dtype=T)
         d_qkvw = ops.linear_wgrad(dqkv, h1, out=_gout(qkvw))
         d_qkvb = ops.colsum(dqkv, out=_gout(qkvb))
         dx = torch.empty(M, D, dtype=torch.float32, device=dxo.device)

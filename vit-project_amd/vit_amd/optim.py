@@ -47,6 +47,10 @@ class _MultiTensor:
         key = tuple(tuple(0 if v is None else int(v) for v in e) for e in entries)
         if key == self._key:
             return
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("optimizer tensor table changed during HIP-graph capture: enable "
+                               "model.use_flat_grads() so gradient addresses are fixed, and warm up once "
+                               "before capturing")
         t = _table(entries, 5)
         chunks = []
         for i, n in enumerate(sizes):
@@ -176,7 +180,9 @@ class FusedAdamW(torch.optim.Optimizer):
                 st["exp_avg_sq"] = torch.zeros_like(p)
                 st["step"] = torch.zeros((), dtype=torch.float32)
             st["step"] += 1
-            entries.append((p.data_ptr(), p.grad.contiguous().data_ptr(), st["exp_avg"].data_ptr(),
+            if not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
+                p.grad = p.grad.float().contiguous()
+            entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
                             st["exp_avg_sq"].data_ptr(), p.numel()))
             sizes.append(p.numel())
         if not entries:
