@@ -21,3 +21,15 @@ for _ in range(reps):
         ops.linear_dgrad(dy, w, out_dtype=bf)
 torch.cuda.synchronize()
 print("done", which)
+if which in ("sdpa_bwd", "sdpa_fwd"):
+    B, H, N = 256, 12, 197
+    qkv = torch.randn(B * N, 3 * 768, device=dev).to(bf)
+    o, lse = ops.sdpa_fwd(qkv, B, H, N)
+    do = torch.randn(B * N, 768, device=dev).to(bf)
+    for _ in range(reps):
+        if which == "sdpa_bwd":
+            ops.sdpa_bwd(qkv, o, do, lse, B, H, N)
+        else:
+            ops.sdpa_fwd(qkv, B, H, N)
+    torch.cuda.synchronize()
+    print("done attn")

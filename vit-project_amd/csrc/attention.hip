@@ -20,19 +20,6 @@
 // of 8 consecutive rows (LDS images).
 __device__ __forceinline__ int at_off(int row, int c) { return row * 128 + ((c ^ (row & 6)) << 4); }
 
-__device__ __forceinline__ bf16x8 at_row_frag(const char* img, int row0, int kk, int lane) {
-  return *reinterpret_cast<const bf16x8*>(img + at_off(row0 + (lane & 15), kk * 4 + (lane >> 4)));
-}
-// transposed fragment: rows (keys/queries) row0 + pi(8g+e), columns d0..d0+15.
-__device__ __forceinline__ bf16x8 at_tr_frag(const char* img, int row0, int d0, int lane) {
-  int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  int c = (d0 >> 3) + (p >> 1);
-  int ra = row0 + 4 * g + q, rb = ra + 16;
-  bf16x4 lo = lds_read_tr(img + at_off(ra, c) + (p & 1) * 8);
-  bf16x4 hi = lds_read_tr(img + at_off(rb, c) + (p & 1) * 8);
-  return cat4(lo, hi);
-}
-
 // Load rows [0, N) of NM head slices (64 wide) into LDS images of ROWS rows,
 // zero-filling rows >= N.  All global loads of the thread are issued before the
 // first LDS write (one latency, not one per chunk); rows >= N load a clamped
@@ -78,6 +65,33 @@ constexpr float LOG2E = 1.4426950408889634f;
 constexpr float LN2 = 0.6931471805599453f;
 
 // ---------------------------------------------------------------------------
+// Per-lane LDS offsets.  Tiles start at multiples of 16 (row fragments) or 32
+// (transposed fragments) rows, which leaves (row & 6) -- the swizzle -- a
+// function of the lane only, so every fragment address is a lane constant plus
+// a wave-uniform tile offset (row0 * 128).
+// ---------------------------------------------------------------------------
+struct AtOffsets {
+  int row[2];   // row fragment, k-substep kk (d 0..31 / 32..63)
+  int tr[4];    // transposed fragment, d-tile dt, rows 4g+q (+16 rows: + 2048)
+  __device__ __forceinline__ AtOffsets(int lane) {
+    const int l15 = lane & 15, g = lane >> 4, q = l15 >> 2, p = l15 & 3;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) row[kk] = l15 * 128 + (((kk * 4 + g) ^ (l15 & 6)) << 4);
+    const int ra = 4 * g + q;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) tr[dt] = ra * 128 + (((2 * dt + (p >> 1)) ^ (ra & 6)) << 4) + (p & 1) * 8;
+  }
+};
+__device__ __forceinline__ bf16x8 rowf(const char* img, int row0, int off) {
+  return *reinterpret_cast<const bf16x8*>(img + row0 * 128 + off);
+}
+__device__ __forceinline__ bf16x8 trf(const char* img, int row0, int off) {
+  const char* b = img + row0 * 128 + off;
+  return cat4(lds_read_tr(b), lds_read_tr(b + 16 * 128));
+}
+__device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// ---------------------------------------------------------------------------
 // bf16 forward
 // ---------------------------------------------------------------------------
 template <int NT>  // key/query tiles of 16: NT = ceil(N/16)
@@ -97,41 +111,42 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
     const int64_t lds_[2] = {ld_qkv, ld_qkv};
     at_load<ROWS, AT_THREADS, 2>(imgs, srcs, lds_, N);
   }
+  const AtOffsets off(lane);
   __syncthreads();
   const float c2 = scale * LOG2E;
   for (int qt = wave; qt < NT; qt += AT_WAVES) {
     const int q = qt * 16 + (lane & 15);
     bf16x8 qf[2];
+    {
+      const int qq = min(q, N - 1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      if (q < N) qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)q * ld_qkv + kk * 32 + g * 8);
-      else { for (int t = 0; t < 8; ++t) qf[kk][t] = (bf16)0.f; }
+      for (int kk = 0; kk < 2; ++kk) qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)qq * ld_qkv + kk * 32 + g * 8);
     }
     f32x4 s[NT];
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt) {
       s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int kk = 0; kk < 2; ++kk) s[kt] = mfma16(at_row_frag(Kimg, kt * 16, kk, lane), qf[kk], s[kt]);
+      for (int kk = 0; kk < 2; ++kk) s[kt] = mfma16(rowf(Kimg, kt * 16, off.row[kk]), qf[kk], s[kt]);
       if (kt % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound K-fragment hoisting (VGPRs)
     }
+    // keys >= N exist only in the last tile
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if ((NT - 1) * 16 + 4 * g + r >= N) s[NT - 1][r] = -INFINITY;
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int key = kt * 16 + 4 * g + r;
-        float v = (key < N) ? s[kt][r] * c2 : -INFINITY;
-        s[kt][r] = v;
-        m = fmaxf(m, v);
-      }
+      for (int r = 0; r < 4; ++r) m = fmaxf(m, s[kt][r]);
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float mc = m * c2;
     float l = 0.f;
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { float p = exp2f(s[kt][r] - m); s[kt][r] = p; l += p; }
+      for (int r = 0; r < 4; ++r) { float p = fexp2(fmaf(s[kt][r], c2, -mc)); s[kt][r] = p; l += p; }
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     f32x4 oacc[4];
@@ -142,7 +157,7 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
       f32x4 hi = (2 * ks + 1 < NT) ? s[2 * ks + 1 < NT ? 2 * ks + 1 : 0] : f32x4{0.f, 0.f, 0.f, 0.f};
       bf16x8 pf = pack8(s[2 * ks], hi);
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma16(at_tr_frag(Vimg, ks * 32, dt * 16, lane), pf, oacc[dt]);
+      for (int dt = 0; dt < 4; ++dt) oacc[dt] = mfma16(trf(Vimg, ks * 32, off.tr[dt]), pf, oacc[dt]);
       if (ks % 2 == 1) __builtin_amdgcn_sched_barrier(0);  // bound V-fragment hoisting (VGPRs)
     }
     if (q < N) {
@@ -154,26 +169,108 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
                      (bf16)(oacc[dt][3] * inv)};
         *reinterpret_cast<bf16x4*>(orow + dt * 16 + 4 * g) = ov;
       }
-      if (g == 0) lse[(int64_t)bh * N + q] = (m + log2f(l)) * LN2;
+      if (g == 0) lse[(int64_t)bh * N + q] = (mc + __log2f(l)) * LN2;
     }
   }
 }
 
 // ---------------------------------------------------------------------------
-// bf16 backward: phase 1 key-parallel (dK, dV), phase 2 query-parallel (dQ).
+// bf16 backward, two kernels per (b, h) so each holds only half the head in LDS
+// (57 KiB -> two workgroups per CU):
+//   attn_bwd_dq  : LDS K, V; each wave owns query tiles (Q, dO, O from global),
+//                  computes delta = rowsum(dO*O) (written for the other kernel),
+//                  recomputes S^T, dP^T over all keys, accumulates dQ.
+//   attn_bwd_dkv : LDS Q, dO (+ lse, delta); each wave owns key tiles (K, V from
+//                  global), recomputes S, dP over all queries, accumulates dK, dV.
 // ---------------------------------------------------------------------------
 template <int NT>
-__global__ __launch_bounds__(AT_THREADS) void attn_bwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H,
-                                                     int N, float scale, const bf16* __restrict__ o, int64_t ld_o,
-                                                     const bf16* __restrict__ dout, int64_t ld_do,
-                                                     const float* __restrict__ lse, const float* __restrict__ delta_in,
-                                                     bf16* __restrict__ dqkv, int64_t ld_dqkv) {
+__global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dq(const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                            int N, float scale, const bf16* __restrict__ o,
+                                                            int64_t ld_o, const bf16* __restrict__ dout, int64_t ld_do,
+                                                            const float* __restrict__ lse, float* __restrict__ delta_out,
+                                                            bf16* __restrict__ dqkv, int64_t ld_dqkv) {
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Qimg = smem;
-  char* Kimg = Qimg + ROWS * 128;
+  __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128];
+  char* Kimg = smem;
   char* Vimg = Kimg + ROWS * 128;
-  char* Oimg = Vimg + ROWS * 128;  // dO
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  const bf16* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  {
+    char* const imgs[2] = {Kimg, Vimg};
+    const bf16* const srcs[2] = {base + D, base + 2 * D};
+    const int64_t lds_[2] = {ld_qkv, ld_qkv};
+    at_load<ROWS, AT_THREADS, 2>(imgs, srcs, lds_, N);
+  }
+  const AtOffsets off(lane);
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  for (int qt = wave; qt < NT; qt += AT_WAVES) {
+    const int q = qt * 16 + (lane & 15);
+    const int qc = min(q, N - 1);
+    bf16x8 qf[2], of[2];
+    float dl = 0.f;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      qf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)qc * ld_qkv + kk * 32 + g * 8);
+      of[kk] = *reinterpret_cast<const bf16x8*>(dout + ((int64_t)b * N + qc) * ld_do + h * 64 + kk * 32 + g * 8);
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(o + ((int64_t)b * N + qc) * ld_o + h * 64 + kk * 32 + g * 8);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) dl = fmaf((float)of[kk][e], (float)ov[e], dl);
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    const float l2 = lse[(int64_t)bh * N + qc] * LOG2E;
+    if (g == 0 && q < N) delta_out[(int64_t)bh * N + q] = dl;
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int kp = 0; kp < NT2; ++kp) {
+      f32x4 ds[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int kt = 2 * kp + u;
+        f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dpacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+          sacc = mfma16(rowf(Kimg, kt * 16, off.row[kk]), qf[kk], sacc);
+          dpacc = mfma16(rowf(Vimg, kt * 16, off.row[kk]), of[kk], dpacc);
+        }
+        const bool edge = (kt + 1) * 16 > N;  // wave-uniform: only the last tiles hold padded keys
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float pv = fexp2(fmaf(sacc[r], c2, -l2));
+          if (edge && kt * 16 + 4 * g + r >= N) pv = 0.f;
+          ds[u][r] = pv * (dpacc[r] - dl);
+        }
+      }
+      const bf16x8 dsf = pack8(ds[0], ds[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(trf(Kimg, kp * 32, off.tr[dt]), dsf, dq[dt]);
+    }
+    if (q < N) {
+      bf16* row = dqkv + ((int64_t)b * N + q) * ld_dqkv + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 qv = {(bf16)(dq[dt][0] * scale), (bf16)(dq[dt][1] * scale), (bf16)(dq[dt][2] * scale),
+                     (bf16)(dq[dt][3] * scale)};
+        *reinterpret_cast<bf16x4*>(row + dt * 16 + 4 * g) = qv;
+      }
+    }
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                             int N, float scale, const bf16* __restrict__ dout,
+                                                             int64_t ld_do, const float* __restrict__ lse,
+                                                             const float* __restrict__ delta_in, bf16* __restrict__ dqkv,
+                                                             int64_t ld_dqkv) {
+  constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
+  __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128 + 2 * ROWS * 4];
+  char* Qimg = smem;
+  char* Oimg = Qimg + ROWS * 128;  // dO
   float* lse2 = reinterpret_cast<float*>(Oimg + ROWS * 128);
   float* delta = lse2 + ROWS;
   const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
@@ -181,33 +278,27 @@ __global__ __launch_bounds__(AT_THREADS) void attn_bwd_mfma(const bf16* __restri
   const bf16* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
   const bf16* dob = dout + (int64_t)b * N * ld_do + h * 64;
   {
-    char* const imgs[2] = {Qimg, Kimg};
-    const bf16* const srcs[2] = {base, base + D};
-    const int64_t lds_[2] = {ld_qkv, ld_qkv};
-    at_load<ROWS, AT_THREADS, 2>(imgs, srcs, lds_, N);
-  }
-  {
-    char* const imgs[2] = {Vimg, Oimg};
-    const bf16* const srcs[2] = {base + 2 * D, dob};
+    char* const imgs[2] = {Qimg, Oimg};
+    const bf16* const srcs[2] = {base, dob};
     const int64_t lds_[2] = {ld_qkv, ld_do};
     at_load<ROWS, AT_THREADS, 2>(imgs, srcs, lds_, N);
   }
-  // per-query constants: delta[q] = sum_d dO*O (precomputed, attn_delta_kernel), lse in log2 units
   for (int q = threadIdx.x; q < ROWS; q += AT_THREADS) {
     delta[q] = (q < N) ? delta_in[(int64_t)bh * N + q] : 0.f;
     lse2[q] = (q < N) ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
   }
+  const AtOffsets off(lane);
   __syncthreads();
   const float c2 = scale * LOG2E;
-
-  // ---- phase 1: key tiles -> dK, dV
   for (int kt = wave; kt < NT; kt += AT_WAVES) {
     const int key = kt * 16 + (lane & 15);
+    const bool kvalid = key < N;
+    const int kc = min(key, N - 1);
     bf16x8 kf[2], vf[2];
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      kf[kk] = at_row_frag(Kimg, kt * 16, kk, lane);
-      vf[kk] = at_row_frag(Vimg, kt * 16, kk, lane);
+      kf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)kc * ld_qkv + D + kk * 32 + g * 8);
+      vf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)kc * ld_qkv + 2 * D + kk * 32 + g * 8);
     }
     f32x4 dv[4], dk[4];
 #pragma unroll
@@ -221,25 +312,26 @@ __global__ __launch_bounds__(AT_THREADS) void attn_bwd_mfma(const bf16* __restri
         f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dpacc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
-          sacc = mfma16(at_row_frag(Qimg, qt * 16, kk, lane), kf[kk], sacc);
-          dpacc = mfma16(at_row_frag(Oimg, qt * 16, kk, lane), vf[kk], dpacc);
+          sacc = mfma16(rowf(Qimg, qt * 16, off.row[kk]), kf[kk], sacc);
+          dpacc = mfma16(rowf(Oimg, qt * 16, off.row[kk]), vf[kk], dpacc);
         }
+        const f32x4 l2 = *reinterpret_cast<const f32x4*>(lse2 + qt * 16 + 4 * g);
+        const f32x4 dl = *reinterpret_cast<const f32x4*>(delta + qt * 16 + 4 * g);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          int qq = qt * 16 + 4 * g + r;
-          float pv = (key < N) ? exp2f(sacc[r] * c2 - lse2[qq]) : 0.f;
+          const float pv = kvalid ? fexp2(fmaf(sacc[r], c2, -l2[r])) : 0.f;
           p[u][r] = pv;
-          ds[u][r] = pv * (dpacc[r] - delta[qq]);
+          ds[u][r] = pv * (dpacc[r] - dl[r]);
         }
       }
-      bf16x8 pf = pack8(p[0], p[1]), dsf = pack8(ds[0], ds[1]);
+      const bf16x8 pf = pack8(p[0], p[1]), dsf = pack8(ds[0], ds[1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        dv[dt] = mfma16(at_tr_frag(Oimg, qp * 32, dt * 16, lane), pf, dv[dt]);
-        dk[dt] = mfma16(at_tr_frag(Qimg, qp * 32, dt * 16, lane), dsf, dk[dt]);
+        dv[dt] = mfma16(trf(Oimg, qp * 32, off.tr[dt]), pf, dv[dt]);
+        dk[dt] = mfma16(trf(Qimg, qp * 32, off.tr[dt]), dsf, dk[dt]);
       }
     }
-    if (key < N) {
+    if (kvalid) {
       bf16* row = dqkv + ((int64_t)b * N + key) * ld_dqkv + h * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
@@ -248,53 +340,6 @@ __global__ __launch_bounds__(AT_THREADS) void attn_bwd_mfma(const bf16* __restri
         bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
         *reinterpret_cast<bf16x4*>(row + D + dt * 16 + 4 * g) = kv;
         *reinterpret_cast<bf16x4*>(row + 2 * D + dt * 16 + 4 * g) = vv;
-      }
-    }
-  }
-
-  // ---- phase 2: query tiles -> dQ
-  for (int qt = wave; qt < NT; qt += AT_WAVES) {
-    const int q = qt * 16 + (lane & 15);
-    bf16x8 qf[2], of[2];
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      qf[kk] = at_row_frag(Qimg, qt * 16, kk, lane);
-      of[kk] = at_row_frag(Oimg, qt * 16, kk, lane);
-    }
-    const float l2 = lse2[q], dl = delta[q];
-    f32x4 dq[4];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int kp = 0; kp < NT2; ++kp) {
-      f32x4 ds[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int kt = 2 * kp + u;
-        f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dpacc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-          sacc = mfma16(at_row_frag(Kimg, kt * 16, kk, lane), qf[kk], sacc);
-          dpacc = mfma16(at_row_frag(Vimg, kt * 16, kk, lane), of[kk], dpacc);
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int key = kt * 16 + 4 * g + r;
-          float pv = (key < N) ? exp2f(sacc[r] * c2 - l2) : 0.f;
-          ds[u][r] = pv * (dpacc[r] - dl);
-        }
-      }
-      bf16x8 dsf = pack8(ds[0], ds[1]);
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(at_tr_frag(Kimg, kp * 32, dt * 16, lane), dsf, dq[dt]);
-    }
-    if (q < N) {
-      bf16* row = dqkv + ((int64_t)b * N + q) * ld_dqkv + h * 64;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        bf16x4 qv = {(bf16)(dq[dt][0] * scale), (bf16)(dq[dt][1] * scale), (bf16)(dq[dt][2] * scale),
-                     (bf16)(dq[dt][3] * scale)};
-        *reinterpret_cast<bf16x4*>(row + dt * 16 + 4 * g) = qv;
       }
     }
   }
@@ -493,17 +538,13 @@ static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N,
 }
 template <int NT>
 static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, const void* o,
-                    int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, const float* delta,
+                    int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, float* delta,
                     void* dqkv, int64_t ld_dqkv, hipStream_t s) {
-  constexpr int ROWS = ((NT + 1) / 2) * 32;
-  size_t lds = 4 * ROWS * 128 + 2 * ROWS * sizeof(float);
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute((const void*)attn_bwd_mfma<NT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((attn_bwd_mfma<NT>), dim3(B * H), dim3(AT_THREADS), lds, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
+  hipLaunchKernelGGL((attn_bwd_dq<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
                      (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, delta, (bf16*)dqkv, ld_dqkv);
+  VIT_CHECK_LAUNCH();
+  hipLaunchKernelGGL((attn_bwd_dkv<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
+                     (const bf16*)dout, ld_do, lse, (const float*)delta, (bf16*)dqkv, ld_dqkv);
   VIT_CHECK_LAUNCH();
   return 0;
 }
@@ -547,10 +588,6 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
   const int D = H * 64;
   if (!delta_ws) return (int)hipErrorInvalidValue;
   if (dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_do % 8 == 0) && (ld_dqkv % 4 == 0) && (ld_o % 4 == 0)) {
-    const int64_t pairs = (int64_t)B * N * H;
-    hipLaunchKernelGGL(attn_delta_kernel<bf16>, dim3((unsigned)((pairs + 15) / 16)), dim3(256), 0, s, (const bf16*)o,
-                       ld_o, (const bf16*)dout, ld_do, B, H, N, delta_ws);
-    VIT_CHECK_LAUNCH();
     int nt = (N + 15) / 16;
     switch (nt) {
 #define CASE(n) case n: return bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, s);
