@@ -66,6 +66,17 @@ def cpu_baseline(seconds: float):
                       f"{el:.1f} s, torch CPU {threads} threads"}
 
 
+def _pmc_traffic():
+    """HBM bytes per launch of the roofline kernel from the committed counter passes
+    (tools/pmc_traffic.py; FETCH_SIZE doubled per the gfx950 correction), or None."""
+    f = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_traffic_fc1_fwd_gelu.json")
+    try:
+        with open(f) as fh:
+            return int(json.load(fh)["traffic_bytes_per_launch"])
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     a = parse()
     import vit_amd
@@ -183,9 +194,12 @@ def main():
                    "model": "vit_base_patch16_224", "global_batch": world * B, "per_gpu_batch": B,
                    "seq_len": 197, "parallelism": f"dp{world}", "launch": "hipgraph" if graph is not None else "eager",
                    "final_loss": round(final_loss, 4)},
-        "roofline": {"bound": "mfma", "kernel": "fast::gemm_kernel fc1 fwd (bias+GELU), M=%d N=3072 K=768" % M,
+        "roofline": {"bound": "mfma", "kernel": "big::gemm_kernel<V5,RC,RC,BIAS_GELU> fc1 fwd, M=%d N=3072 K=768" % M,
                      "achieved": round(k_tflops, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
-                     "frac": round(k_tflops / PEAK_BF16_TFLOPS, 4), "traffic": None,
+                     "frac": round(k_tflops / PEAK_BF16_TFLOPS, 4), "traffic": _pmc_traffic(),
+                     "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc passes, "
+                                     "profiles/r01/pmc_traffic_fc1_fwd_gelu.json)",
+                     "algorithmic_bytes": (M * 768 + 3072 * 768 + 2 * M * 3072) * 2 + 3072 * 4,
                      "kernel_ms": round(k_ms, 4), "flop_per_launch": k_flop},
         "step_mfma": {"achieved_tflops": round(step_tflops, 1), "frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
                       "flop_per_img": STEP_FLOP_PER_IMG},

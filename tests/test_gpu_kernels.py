@@ -105,6 +105,34 @@ def test_linear_wgrad(M, N, K, split):
     _close(dw, ref, 2e-5, "wgrad")
 
 
+@pytest.mark.parametrize("variant", [1, 2, 5, 8, 9])
+def test_gemm_every_tile_config(variant):
+    """Every kept MFMA configuration (forced through vit_gemm_variant) on ragged
+    M/N tiles, fwd + bias/GELU/residual epilogues, dgrad, split-K wgrad."""
+    lib = L.lib()
+    M, N, K = 197 * 3, 640, 448          # M, N not multiples of any tile; K % 64 == 0
+    x = _rnd(M, K, seed=40, dtype=torch.bfloat16)
+    w = _rnd(N, K, seed=41, scale=0.05, dtype=torch.bfloat16)
+    b = _rnd(N, seed=42)
+    res = _rnd(M, N, seed=43)
+    dy = _rnd(M, N, seed=44, dtype=torch.bfloat16)
+    xd, wd, bd, dyd = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
+    lib.vit_gemm_variant(variant)
+    try:
+        ref = x.float() @ w.float().T + b
+        pre, act = ops.linear_fwd(xd, wd, bd, epi=L.EPI_BIAS_GELU)
+        _close(pre, ref, 1e-2, "pre")
+        _close(act, torch.nn.functional.gelu(pre.float().cpu()), 1e-2, "gelu")
+        out = res.to(DEV).clone()
+        ops.linear_fwd(xd, wd, bd, epi=L.EPI_RESID, resid=out, out=out)
+        _close(out, ref + res, 1e-5, "resid")
+        _close(ops.linear_dgrad(dyd, wd), dy.float() @ w.float(), 1e-5, "dgrad")
+        for split in (1, 3):
+            _close(ops.linear_wgrad(dyd, xd, split=split), dy.float().T @ x.float(), 2e-5, f"wgrad split {split}")
+    finally:
+        lib.vit_gemm_variant(-1)
+
+
 def test_gemm_cr_rc_layout_fast():
     # the fourth layout combination (P CR, Q RC) through the raw dispatcher
     M, N, R = 256, 128, 192

@@ -199,3 +199,40 @@ def test_bf16_batch32_matches_oracle_and_graph_replay():
     assert abs(gl.item() - loss.item()) < 1e-3 * abs(loss.item()) + 1e-4
     for (k, a), (_, b) in zip(m.named_parameters(), m2.named_parameters()):
         assert _rel(b, a) < 1e-5, k
+
+
+def test_reference_training_loop_unchanged(golden_dir):
+    """VIT:132-147 as the reference writes it -- DDP wrapper (VIT:287), autocast, GradScaler,
+    torch.optim.SGD (VIT:294-299), torch's F.cross_entropy -- around our model gives the
+    golden step (f32 parity path, 1e-3 relative)."""
+    import socket
+    import torch.distributed as dist
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    fx = torch.load(os.path.join(golden_dir, "vit_tiny_golden.pt"), weights_only=True)
+    cfg = R.ViTConfig(**fx["cfg"])
+    p = R.init_params(cfg, seed=fx["seed"], random_affine=True)
+    x, y = _inputs(cfg, fx["B"], fx["seed"])
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        model = DDP(_model(cfg, p, torch.float32), device_ids=[0])
+        optimizer = torch.optim.SGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
+        scaler = torch.amp.GradScaler("cuda")
+        model.train()
+        images, targets = x.to(DEV, non_blocking=True), y.to(DEV, non_blocking=True)
+        optimizer.zero_grad()
+        with torch.autocast("cuda"):
+            outputs = model(images)
+            loss = torch.nn.functional.cross_entropy(outputs, targets)
+        scaler.scale(loss).backward()
+        scaler.step(optimizer)
+        scaler.update()
+        torch.cuda.synchronize()
+        assert _rel(outputs, fx["logits"]) < 1e-3
+        assert abs(loss.item() - fx["loss"]) < 1e-3 * abs(fx["loss"])
+        for k, v in model.module.state_dict().items():
+            assert _rel(v, fx["params_after"][k]) < 1e-3, k
+    finally:
+        dist.destroy_process_group()

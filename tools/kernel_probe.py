@@ -17,6 +17,17 @@ for _ in range(reps):
         ops.linear_wgrad(dy, x)
     elif which == "fwd_fc1":
         ops.linear_fwd(x, w, None, out_dtype=bf)
+    elif which == "fwd_fc1_gelu":
+        b = torch.zeros(F, device=dev)
+        pre = torch.empty(M, F, device=dev, dtype=bf)
+        act = torch.empty_like(pre)
+        ops.linear_fwd(x, w, b, epi=L.EPI_BIAS_GELU, out=pre, act_out=act)
+    elif which == "ln_fwd":  # calibration: reads M*768*4 B, writes M*768*2 B (+ 8 B/row stats)
+        if _ == 0:
+            xf = torch.randn(M, D, device=dev)
+            lw, lb = torch.ones(D, device=dev), torch.zeros(D, device=dev)
+            y = torch.empty(M, D, device=dev, dtype=bf)
+        ops.layer_norm_fwd(xf, lw, lb, 1e-6, bf, out=y)
     elif which == "dgrad_fc1":
         ops.linear_dgrad(dy, w, out_dtype=bf)
 torch.cuda.synchronize()

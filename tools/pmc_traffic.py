@@ -1,0 +1,53 @@
+"""Per-dispatch HBM traffic of one kernel from rocprofv3 counter CSVs.
+
+    python tools/pmc_traffic.py <dir with *_counter_collection.csv> <kernel-name substring> [--out f.json]
+
+FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB per dispatch.
+Correction applied (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE
+reports half the bytes of a wide coalesced streaming read, so it is doubled;
+WRITE_SIZE is exact for 16-B-per-lane stores.  The calibration kernel
+(ln_fwd in tools/kernel_probe.py, known byte counts) checks both.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def collect(d, sub):
+    vals = defaultdict(list)
+    names = set()
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if sub in row["Kernel_Name"]:
+                    vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
+                    names.add(row["Kernel_Name"][:160])
+    return vals, names
+
+
+def main():
+    d, sub = sys.argv[1], sys.argv[2]
+    out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else None
+    vals, names = collect(d, sub)
+    res = {"kernel_match": sub, "kernels": sorted(names), "dispatches": {k: len(v) for k, v in vals.items()}}
+    for k, v in vals.items():
+        res[k + "_KiB_avg"] = sum(v) / len(v)
+    fetch = res.get("FETCH_SIZE_KiB_avg")
+    write = res.get("WRITE_SIZE_KiB_avg")
+    if fetch is not None:
+        res["fetch_bytes_corrected"] = fetch * 1024 * 2
+    if write is not None:
+        res["write_bytes"] = write * 1024
+    if fetch is not None and write is not None:
+        res["traffic_bytes_per_launch"] = res["fetch_bytes_corrected"] + res["write_bytes"]
+    print(json.dumps(res, indent=1))
+    if out:
+        with open(out, "w") as fh:
+            json.dump(res, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()

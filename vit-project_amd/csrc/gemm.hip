@@ -326,6 +326,143 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
   }
 }
 
+// ----------------------------------------------------------------------------
+// Ping-pong schedule: 256x256 tile, BK = 32, 8 waves in two groups of four
+// (group g owns rows g*128..g*128+127; wave w%4 owns 64 columns).  Each k-tile is
+// two phases -- {ds_read fragments} barrier {MFMA cluster of 16} barrier -- and
+// group 1 runs one barrier behind group 0, so on every SIMD one wave's MFMA
+// cluster overlaps the other wave's LDS reads.  Operands stream through an
+// S-deep ring of 32-KiB stages filled by global_load_lds, S-1 tiles ahead; each
+// tile's loads are split over the two MFMA phases and retired by a counted
+// vmcnt (never 0 inside the loop), raw s_barrier only.
+// ----------------------------------------------------------------------------
+template <int S_> struct PP {
+  static constexpr int S = S_, BM = 256, BN = 256, BK = 32, THREADS = 512;
+  static constexpr int PIMG = BM * BK * 2, STAGE = 2 * PIMG, LDS = S * STAGE;
+  static_assert(LDS <= 163840, "LDS");
+};
+
+// s_waitcnt vmcnt(n) for a wave-uniform even n <= 14
+__device__ __forceinline__ void wait_vm_n(int n) {
+  switch (n) {
+    case 0: wait_vm<0>(); break;
+    case 2: wait_vm<2>(); break;
+    case 4: wait_vm<4>(); break;
+    case 6: wait_vm<6>(); break;
+    case 8: wait_vm<8>(); break;
+    case 10: wait_vm<10>(); break;
+    case 12: wait_vm<12>(); break;
+    default: wait_vm<14>(); break;
+  }
+}
+__device__ __forceinline__ void lgkm_wait0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int S, int PL, int QL, int EPI, typename TO, typename TA>
+__global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, int64_t ldp,
+                                                    const bf16* __restrict__ Q, int64_t ldq,
+                                                    int M, int N, int R, int r_chunk, Epi e) {
+  using C = PP<S>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, wj = wave & 3;
+  const int tiles_j = (N + 255) / 256;
+  const int tiles = ((M + 255) / 256) * tiles_j;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int z = w / tiles, t0 = w - z * tiles;
+  const int ti = t0 / tiles_j, tj = t0 - ti * tiles_j;
+  const int i0 = ti * 256, j0 = tj * 256;
+  const int rb = z * r_chunk;
+  const int re = min(R, rb + r_chunk);
+  const int nk = (re - rb) / 32;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int a = 0; a < 8; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto issueP = [&](int k) {
+    stage<PL, 256, 32, 2>(smem + (k % S) * C::STAGE, P, ldp, i0, rb + k * 32, M, wave, lane);
+  };
+  auto issueQ = [&](int k) {
+    stage<QL, 256, 32, 2>(smem + (k % S) * C::STAGE + C::PIMG, Q, ldq, j0, rb + k * 32, N, wave, lane);
+  };
+  // one k-tile; register sets passed in so consecutive tiles alternate sets (no WAR on
+  // fragments an in-flight MFMA still reads)
+  auto tile = [&](int t, bf16x8 (&qf)[4], bf16x8 (&p0)[4], bf16x8 (&p1)[4]) {
+    const char* cur = smem + (t % S) * C::STAGE;
+    const bool more = t + S - 1 < nk;
+    // phase A: reads
+#pragma unroll
+    for (int b = 0; b < 4; ++b) qf[b] = frag<QL, 256, 32>(cur + C::PIMG, wj * 4 + b, 0, lane);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) p0[a] = frag<PL, 256, 32>(cur, grp * 8 + a, 0, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+    // phase A: MFMA (rows 0..63 of the group's 128)
+    lgkm_wait0();
+    if (more) issueP(t + S - 1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[a][b] = mfma16(qf[b], p0[a], acc[a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+    // phase B: reads; retire tile t+1's loads before the barrier that precedes its first read
+#pragma unroll
+    for (int a = 0; a < 4; ++a) p1[a] = frag<PL, 256, 32>(cur, grp * 8 + 4 + a, 0, lane);
+    if (t + 1 < nk) {  // in flight behind tile t+1: tiles t+2.. (4 loads each) and tile t+S-1's P half
+      if (more) wait_vm<4 * (S - 3) + 2>();
+      else wait_vm_n(4 * (nk - 2 - t));
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+    // phase B: MFMA (rows 64..127)
+    lgkm_wait0();
+    if (more) issueQ(t + S - 1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc[4 + a][b] = mfma16(qf[b], p1[a], acc[4 + a][b]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+    lds_barrier();
+  };
+
+  if (nk > 0) {
+#pragma unroll
+    for (int k = 0; k < S - 1; ++k)
+      if (k < nk) { issueP(k); issueQ(k); }
+    wait_vm_n(4 * min(S - 2, nk - 1));
+    lds_barrier();
+    if (grp) lds_barrier();  // stagger group 1 by one phase
+    bf16x8 qA[4], pA0[4], pA1[4], qB[4], pB0[4], pB1[4];
+    int t = 0;
+    for (; t + 1 < nk; t += 2) {
+      tile(t, qA, pA0, pA1);
+      tile(t + 1, qB, pB0, pB1);
+    }
+    if (t < nk) tile(t, qA, pA0, pA1);
+    if (!grp) lds_barrier();  // rebalance the barrier count
+  }
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    const int i = i0 + grp * 128 + a * 16 + (lane & 15);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const int j = j0 + wj * 64 + b * 16 + 4 * (lane >> 4);
+      if (i < M && j < N) epi4<EPI, TO, TA>(e, i, j, acc[a][b], z);
+    }
+  }
+}
+
 // the configurations kept after the sweep (tools/bench_kernels.py --sweep; DESIGN.md
 // lists the measured TFLOP/s per shape).  Others tried: 256x256x32 S5 with register
 // double-buffering (1 WG/CU; wgrad 360-400 TF), 128x128x32 S4, 256x128x64 S3, 128x256x32 S4.
@@ -454,7 +591,7 @@ static int pick_variant(int pl, int ql, int M, int N, int R, int split) {
   else if (pl == LAY_RC && ql == LAY_RC) v = N >= 1536 ? 5 : 2;
   else v = 1;                                                   // dgrad (r-strided Q)
   (void)M;
-  if (v != 1 && R % 64) v = 1;                                  // BK = 64 configurations need 64-row chunks
+  if ((v == 2 || v == 5) && R % 64) v = 1;                                  // BK = 64 configurations need 64-row chunks
   return v;
 }
 
@@ -482,12 +619,34 @@ static int launch_big(const void* P, int64_t ldp, const void* Q, int64_t ldq, in
   return 0;
 }
 
+template <int S, int PL, int QL, int EPI, typename TO, typename TA>
+static int launch_pp(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
+                     const Epi& e, hipStream_t s) {
+  using C = big::PP<S>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)big::pp_kernel<S, PL, QL, EPI, TO, TA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  if (R % C::BK) return (int)hipErrorInvalidValue;
+  const int r_chunk = r_chunk_for(R, split, 64);
+  const int nz = (R + r_chunk - 1) / r_chunk;
+  dim3 grid(((M + 255) / 256) * ((N + 255) / 256) * nz);
+  hipLaunchKernelGGL((big::pp_kernel<S, PL, QL, EPI, TO, TA>), grid, dim3(C::THREADS), C::LDS, s,
+                     (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, r_chunk, e);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int PL, int QL, int EPI, typename TO, typename TA>
 static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R,
                        int split, const Epi& e, hipStream_t s) {
   switch (pick_variant(PL, QL, M, N, R, split)) {
     case 2: return launch_big<big::V2, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 5: return launch_big<big::V5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    case 8: return launch_pp<4, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    case 9: return launch_pp<5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     default: return launch_big<big::V1, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
   }
 }
