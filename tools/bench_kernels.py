@@ -130,6 +130,20 @@ def sweep(a, variants):
         cases.append((f"fwd_{nm}", flop, lambda x=x, w=w, o=outb: ops.linear_fwd(x, w, None, out=o), outb))
         cases.append((f"dgrad_{nm}", flop, lambda dy=dy, w=w, o=dxb: ops.linear_dgrad(dy, w, out=o), dxb))
         cases.append((f"wgrad_{nm}", flop, lambda dy=dy, x=x, o=dw: ops.linear_wgrad(dy, x, out=o), dw))
+        if nm == "fc1":
+            act = torch.empty_like(outb)
+            b1 = torch.randn(Nout, device=dev)
+            cases.append(("fwd_fc1_gelu", flop, lambda x=x, w=w, o=outb, a_=act, b_=b1:
+                          ops.linear_fwd(x, w, b_, epi=L.EPI_BIAS_GELU, out=o, act_out=a_), act))
+        if nm in ("proj", "fc2"):
+            res = torch.randn(M, Nout, device=dev)
+            cases.append((f"fwd_{nm}_resid", flop, lambda x=x, w=w, r_=res:
+                          ops.linear_fwd(x, w, None, epi=L.EPI_RESID, resid=r_, out=r_), res))
+        if nm == "fc2":
+            pre = r(M, K)
+            dxg = torch.empty(M, K, device=dev, dtype=bf)
+            cases.append(("dgrad_fc2_gelubwd", flop, lambda dy=dy, w=w, p_=pre, o=dxg:
+                          ops.linear_dgrad(dy, w, out_dtype=bf, epi=L.EPI_GELU_BWD, pre=p_, out=o), dxg))
     lib = L.lib()
     ref = {}
     lib.vit_gemm_variant(-1)
@@ -140,7 +154,7 @@ def sweep(a, variants):
         lib.vit_gemm_variant(v)
         for name, flop, fn, out in cases:
             t = timeit(fn, a.reps)
-            err = ((out.float() - ref[name]).abs().max() / ref[name].abs().max()).item()
+            err = ((out.float() - ref[name]).abs().max() / ref[name].abs().max()).item() if "resid" not in name else 0.0
             table.setdefault(name, {})[v] = round(flop / t / 1e12, 1)
             print(json.dumps({"variant": v, "name": name, "ms": round(t * 1e3, 4), "tflops": round(flop / t / 1e12, 1),
                               "max_rel_vs_default": round(err, 6)}), flush=True)

@@ -6,6 +6,8 @@ import torch
 from vit_amd import ops, _lib as L
 which = sys.argv[1] if len(sys.argv) > 1 else "wgrad_fc1"
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+if len(sys.argv) > 3:  # force a GEMM tile configuration (big::V<n> / ping-pong 8, 9)
+    L.lib().vit_gemm_variant(int(sys.argv[3]))
 M, D, F = 256 * 197, 768, 3072
 bf = torch.bfloat16
 dev = "cuda"
@@ -15,6 +17,11 @@ w = (torch.randn(F, D, device=dev) * 0.05).to(bf)
 for _ in range(reps):
     if which == "wgrad_fc1":
         ops.linear_wgrad(dy, x)
+    elif which == "fwd_fc2":
+        if _ == 0:
+            a2 = torch.randn(M, F, device=dev).to(bf)
+            w2 = (torch.randn(D, F, device=dev) * 0.05).to(bf)
+        ops.linear_fwd(a2, w2, None, out_dtype=bf)
     elif which == "fwd_fc1":
         ops.linear_fwd(x, w, None, out_dtype=bf)
     elif which == "fwd_fc1_gelu":

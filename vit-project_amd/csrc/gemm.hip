@@ -20,6 +20,7 @@
 #include "common.hpp"
 #include "reduce.hpp"
 #include <string.h>
+#include <type_traits>
 
 enum { LAY_RC = 0, LAY_CR = 1 };
 enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_PATCH = 4,
@@ -33,6 +34,7 @@ struct Epi {
   const float* pos;         // EPI_PATCH: pos_embed [seq, N]
   int n_patch;              // EPI_PATCH: patches per image (seq = n_patch + 1)
   int64_t slab;             // split-r: element offset of slab z
+  int dbg;                  // timing experiments only (vit_gemm_variant(v + 100*bits)): 1 = no in-loop loads, 2 = no in-loop barriers
 };
 
 template <typename T> __device__ __forceinline__ void store4(T* p, f32x4 v);
@@ -199,6 +201,39 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int s, int kk, int lane)
     const int r0 = kk * 32 + 8 * g + q;
     bf16x4 lo = lds_read_tr(img + cr_off<ROWS>(r0, c) + (p & 1) * 8);
     bf16x4 hi = lds_read_tr(img + cr_off<ROWS>(r0 + 4, c) + (p & 1) * 8);
+    return cat4(lo, hi);
+  }
+}
+
+// Fragment reads as inline asm: the compiler cannot see them as LDS reads, so it
+// does not put an s_waitcnt vmcnt(0) (for the in-flight global_load_lds writes it
+// cannot prove disjoint) in front of them.  The caller orders them: a counted
+// vmcnt + barrier before (data landed), lgkm_wait0() before the first use.
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+  return (uint32_t)(uintptr_t)LDS_PTR(p);
+}
+__device__ __forceinline__ bf16x8 asm_read128(uint32_t a) {
+  i32x4 v;
+  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ bf16x4 asm_read_tr(uint32_t a) {
+  i32x2 v;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+  return __builtin_bit_cast(bf16x4, v);
+}
+template <int LAY, int ROWS, int BK>
+__device__ __forceinline__ bf16x8 frag_asm(uint32_t img, int s, int kk, int lane) {
+  if constexpr (LAY == LAY_RC) {
+    return asm_read128(img + rc_off<BK>(s * 16 + (lane & 15), kk * 4 + (lane >> 4)));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int c = 2 * s + (p >> 1);
+    const int r0 = kk * 32 + 8 * g + q;
+    bf16x4 lo = asm_read_tr(img + cr_off<ROWS>(r0, c) + (p & 1) * 8);
+    bf16x4 hi = asm_read_tr(img + cr_off<ROWS>(r0 + 4, c) + (p & 1) * 8);
     return cat4(lo, hi);
   }
 }
@@ -385,27 +420,62 @@ __global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, 
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto issueP = [&](int k) {
-    stage<PL, 256, 32, 2>(smem + (k % S) * C::STAGE, P, ldp, i0, rb + k * 32, M, wave, lane);
+  // per-lane global source pointers of this wave's 4 staging pieces (2 of P, 2 of Q),
+  // advanced by one k-tile after each issue; LDS destination = slot + piece * 1 KiB
+  const bf16* srcP[2];
+  const bf16* srcQ[2];
+  int64_t stepP, stepQ;
+  {
+    auto init = [&](auto lay_tag, const bf16* base, int64_t ld, int row0, int lim, const bf16* (&src)[2],
+                    int64_t& step) {
+      constexpr int LAY = decltype(lay_tag)::value;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = wave * 2 + u;
+        if constexpr (LAY == LAY_RC) {
+          const int row = t * 16 + lane / 4;
+          const int c = (lane % 4) ^ rc_sw<32>(row);
+          src[u] = base + (int64_t)min(row0 + row, lim - 1) * ld + rb + c * 8;
+          step = 32;
+        } else {
+          const int r = t * 2 + lane / 32;
+          const int c = cr_swz(lane % 32, r);
+          src[u] = base + (int64_t)(rb + r) * ld + min(row0 + c * 8, lim - 8);
+          step = 32 * ld;
+        }
+      }
+    };
+    init(std::integral_constant<int, PL>{}, P, ldp, i0, M, srcP, stepP);
+    init(std::integral_constant<int, QL>{}, Q, ldq, j0, N, srcQ, stepQ);
+  }
+  // issue the 4 loads of the next k-tile in sequence into ring slot k % S
+  auto issue = [&](int k) {
+    char* buf = smem + (k % S) * C::STAGE;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      __builtin_amdgcn_global_load_lds((const void*)srcP[u], LDS_PTR(buf + (wave * 2 + u) * 1024), 16, 0, 0);
+      srcP[u] += stepP;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      __builtin_amdgcn_global_load_lds((const void*)srcQ[u], LDS_PTR(buf + C::PIMG + (wave * 2 + u) * 1024), 16, 0, 0);
+      srcQ[u] += stepQ;
+    }
   };
-  auto issueQ = [&](int k) {
-    stage<QL, 256, 32, 2>(smem + (k % S) * C::STAGE + C::PIMG, Q, ldq, j0, rb + k * 32, N, wave, lane);
-  };
-  // one k-tile; register sets passed in so consecutive tiles alternate sets (no WAR on
-  // fragments an in-flight MFMA still reads)
+  const bool dbg_noload = e.dbg & 1, dbg_nobar = e.dbg & 2;
+  auto bar = [&]() { if (!dbg_nobar) lds_barrier(); };
+  // one k-tile = two phases {reads} barrier {16 MFMA} barrier; the next tile's loads are
+  // issued in the second read phase, where the partner wave's MFMAs cover their issue
   auto tile = [&](int t, bf16x8 (&qf)[4], bf16x8 (&p0)[4], bf16x8 (&p1)[4]) {
-    const char* cur = smem + (t % S) * C::STAGE;
-    const bool more = t + S - 1 < nk;
-    // phase A: reads
+    const uint32_t cur = lds_addr(smem + (t % S) * C::STAGE);
+    const bool more = t + S - 1 < nk && !dbg_noload;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) qf[b] = frag<QL, 256, 32>(cur + C::PIMG, wj * 4 + b, 0, lane);
+    for (int b = 0; b < 4; ++b) qf[b] = frag_asm<QL, 256, 32>(cur + C::PIMG, wj * 4 + b, 0, lane);
 #pragma unroll
-    for (int a = 0; a < 4; ++a) p0[a] = frag<PL, 256, 32>(cur, grp * 8 + a, 0, lane);
+    for (int a = 0; a < 4; ++a) p0[a] = frag_asm<PL, 256, 32>(cur, grp * 8 + a, 0, lane);
     __builtin_amdgcn_sched_barrier(0);
-    lds_barrier();
-    // phase A: MFMA (rows 0..63 of the group's 128)
+    bar();
     lgkm_wait0();
-    if (more) issueP(t + S - 1);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -413,19 +483,17 @@ __global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, 
       for (int b = 0; b < 4; ++b) acc[a][b] = mfma16(qf[b], p0[a], acc[a][b]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    lds_barrier();
-    // phase B: reads; retire tile t+1's loads before the barrier that precedes its first read
+    bar();
 #pragma unroll
-    for (int a = 0; a < 4; ++a) p1[a] = frag<PL, 256, 32>(cur, grp * 8 + 4 + a, 0, lane);
-    if (t + 1 < nk) {  // in flight behind tile t+1: tiles t+2.. (4 loads each) and tile t+S-1's P half
-      if (more) wait_vm<4 * (S - 3) + 2>();
+    for (int a = 0; a < 4; ++a) p1[a] = frag_asm<PL, 256, 32>(cur, grp * 8 + 4 + a, 0, lane);
+    if (t + 1 < nk && !dbg_noload) {  // tile t+1 landed; in flight behind it: tiles t+2.. (4 loads each)
+      if (t + S - 2 < nk) wait_vm<4 * (S - 3)>();
       else wait_vm_n(4 * (nk - 2 - t));
     }
+    if (more) issue(t + S - 1);  // slot (t-1) % S: every wave's reads of tile t-1 retired two phases ago
     __builtin_amdgcn_sched_barrier(0);
-    lds_barrier();
-    // phase B: MFMA (rows 64..127)
+    bar();
     lgkm_wait0();
-    if (more) issueQ(t + S - 1);
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int a = 0; a < 4; ++a)
@@ -433,13 +501,13 @@ __global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, 
       for (int b = 0; b < 4; ++b) acc[4 + a][b] = mfma16(qf[b], p1[a], acc[4 + a][b]);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
-    lds_barrier();
+    bar();
   };
 
   if (nk > 0) {
 #pragma unroll
     for (int k = 0; k < S - 1; ++k)
-      if (k < nk) { issueP(k); issueQ(k); }
+      if (k < nk) issue(k);
     wait_vm_n(4 * min(S - 2, nk - 1));
     lds_barrier();
     if (grp) lds_barrier();  // stagger group 1 by one phase
@@ -581,15 +649,16 @@ static bool fast_ok(int dtype, int M, int N, int R, const void* P, const void* Q
   return true;
 }
 
-static int g_variant = -1;  // -1: per-shape choice; 1, 2, 5: force big::V<n> (tuning)
+static int g_variant = -1;  // -1: per-shape choice; 1, 2, 5: force big::V<n>, 8, 9: ping-pong (tuning)
+static int g_dbg = 0;
 
 // per-shape choice among the kept configurations (sweep on MI355X, bs=256 ViT-B/16 shapes)
 static int pick_variant(int pl, int ql, int M, int N, int R, int split) {
   int v;
-  if (g_variant >= 0) v = g_variant;
-  else if (split > 1 || (pl == LAY_CR && ql == LAY_CR)) v = 5;  // wgrad: 256x256 tiles, split-K sized for them
-  else if (pl == LAY_RC && ql == LAY_RC) v = N >= 1536 ? 5 : 2;
-  else v = 1;                                                   // dgrad (r-strided Q)
+  if (g_variant >= 0) v = g_variant % 100;
+  else if (split > 1 || (pl == LAY_CR && ql == LAY_CR)) v = 8;  // wgrad: ping-pong 256x256, split-K sized for it
+  else if (pl == LAY_RC && ql == LAY_RC) v = N >= 1536 ? 5 : 2; // forward: K = 768 is too short for ping-pong
+  else v = (N <= 1024 && R <= 1024) ? 2 : 8;                    // dgrad
   (void)M;
   if ((v == 2 || v == 5) && R % 64) v = 1;                                  // BK = 64 configurations need 64-row chunks
   return v;
@@ -708,12 +777,12 @@ static int gemm_any(int epi, int dtype, int out_dtype, int pl, int ql, int M, in
   return (int)hipErrorInvalidValue;
 }
 
-static Epi make_epi() { Epi e; memset(&e, 0, sizeof(e)); return e; }
+static Epi make_epi() { Epi e; memset(&e, 0, sizeof(e)); e.dbg = g_dbg; return e; }
 
 extern "C" {
 
 // Tuning hook: force GEMM configuration big::V<v> (-1 restores the per-shape heuristic).
-int vit_gemm_variant(int v) { g_variant = v; return 0; }
+int vit_gemm_variant(int v) { g_variant = v; g_dbg = v >= 100 ? v / 100 : 0; return 0; }
 
 // Raw dispatcher (exported for tests/benchmarks of individual layouts).
 int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int M, int N, int R,
