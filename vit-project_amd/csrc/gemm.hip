@@ -34,7 +34,7 @@ struct Epi {
   const float* pos;         // EPI_PATCH: pos_embed [seq, N]
   int n_patch;              // EPI_PATCH: patches per image (seq = n_patch + 1)
   int64_t slab;             // split-r: element offset of slab z
-  int dbg;                  // timing experiments only (vit_gemm_variant(v + 100*bits)): 1 = no in-loop loads, 2 = no in-loop barriers
+  int dbg;                  // timing experiments only (vit_gemm_variant(v + 100*bits)): 1 = no in-loop loads, 2 = no in-loop barriers, 4 = no epilogue
 };
 
 template <typename T> __device__ __forceinline__ void store4(T* p, f32x4 v);
@@ -238,6 +238,11 @@ __device__ __forceinline__ bf16x8 frag_asm(uint32_t img, int s, int kk, int lane
   }
 }
 
+__device__ __forceinline__ void lgkm_wait0() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   // bijective: blocks that share an XCD (bid % 8) get a contiguous range of ids
   int xcd = bid & 7, q = nwg >> 3, r = nwg & 7, k = bid >> 3;
@@ -319,8 +324,15 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
         if (kt + S - 1 < nk) issue(kt + S - 1);
 #pragma unroll
         for (int kk = 0; kk < C::KS; ++kk) {
+          // asm fragment reads (no compiler vmcnt(0) for the in-flight ring loads);
+          // retired before the MFMAs, so they are also done before the next barrier (WAR)
+          const uint32_t cur = lds_addr(smem + (kt % S) * C::STAGE);
           bf16x8 pf[C::AI], qf[C::AJ];
-          load_frags(kt, kk, pf, qf);
+#pragma unroll
+          for (int b = 0; b < C::AJ; ++b) qf[b] = frag_asm<QL, BN, BK>(cur + C::PIMG, wj * C::AJ + b, kk, lane);
+#pragma unroll
+          for (int a = 0; a < C::AI; ++a) pf[a] = frag_asm<PL, BM, BK>(cur, wi * C::AI + a, kk, lane);
+          lgkm_wait0();
           mma(pf, qf);
         }
       }
@@ -348,6 +360,13 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
       }
       if (kt < nk) step(kt, pA, qA, pB, qB);
     }
+  }
+  if (e.dbg & 4) {  // timing experiment: keep the accumulators live, skip the epilogue
+#pragma unroll
+    for (int a = 0; a < C::AI; ++a)
+#pragma unroll
+      for (int b = 0; b < C::AJ; ++b) asm volatile("" ::"v"(acc[a][b]));
+    return;
   }
   // epilogue: acc[a][b] holds C[i][j..j+3] with i = lane&15, j = 4*(lane>>4)
 #pragma unroll
@@ -389,10 +408,6 @@ __device__ __forceinline__ void wait_vm_n(int n) {
     case 12: wait_vm<12>(); break;
     default: wait_vm<14>(); break;
   }
-}
-__device__ __forceinline__ void lgkm_wait0() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
 }
 
 template <int S, int PL, int QL, int EPI, typename TO, typename TA>
@@ -520,6 +535,13 @@ __global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, 
     if (t < nk) tile(t, qA, pA0, pA1);
     if (!grp) lds_barrier();  // rebalance the barrier count
   }
+  if (e.dbg & 4) {
+#pragma unroll
+    for (int a = 0; a < 8; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     const int i = i0 + grp * 128 + a * 16 + (lane & 15);
@@ -538,6 +560,8 @@ __global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, 
 using V1 = Cfg<256, 128, 32, 4, 2, 3, false, 4>;  //  72 KiB, 2 WG/CU: dgrad
 using V2 = Cfg<128, 128, 64, 2, 2, 2, false, 2>;  //  64 KiB, 2 WG/CU (4 waves): N = 768 forward
 using V5 = Cfg<256, 256, 64, 2, 4, 2, false, 2>;  // 128 KiB, 1 WG/CU: wide forward, wgrad
+using V3 = Cfg<128, 256, 32, 2, 2, 3, false, 2>;  //  72 KiB, 2 WG/CU (4 waves of 64x128)
+using V4 = Cfg<256, 128, 32, 4, 2, 4, false, 4>;  //  96 KiB, 1 WG/CU, 4-deep ring
 }  // namespace big
 
 // ----------------------------------------------------------------------------
@@ -714,6 +738,8 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
   switch (pick_variant(PL, QL, M, N, R, split)) {
     case 2: return launch_big<big::V2, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 5: return launch_big<big::V5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    case 3: return launch_big<big::V3, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    case 4: return launch_big<big::V4, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 8: return launch_pp<4, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 9: return launch_pp<5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     default: return launch_big<big::V1, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
