@@ -38,6 +38,7 @@ def parse():
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per step")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true", help="weight gradients inline instead of on a side stream")
     return ap.parse_args()
 
 
@@ -93,6 +94,7 @@ def main():
     B = a.batch
     model = vit_amd.create_model("vit_base_patch16_224", num_classes=1000, compute_dtype=torch.bfloat16).to(dev)
     flat = model.use_flat_grads(True)
+    vit_amd.set_wgrad_overlap(not a.no_overlap)
     opt = vit_amd.FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     x = torch.randn(B, 3, 224, 224, device=dev)
     y = torch.randint(0, 1000, (B,), device=dev)

@@ -680,9 +680,9 @@ static int g_dbg = 0;
 static int pick_variant(int pl, int ql, int M, int N, int R, int split) {
   int v;
   if (g_variant >= 0) v = g_variant % 100;
-  else if (split > 1 || (pl == LAY_CR && ql == LAY_CR)) v = 8;  // wgrad: ping-pong 256x256, split-K sized for it
-  else if (pl == LAY_RC && ql == LAY_RC) v = N >= 1536 ? 5 : 2; // forward: K = 768 is too short for ping-pong
-  else v = (N <= 1024 && R <= 1024) ? 2 : 8;                    // dgrad
+  else if (split > 1 || (pl == LAY_CR && ql == LAY_CR)) v = 8;           // wgrad: ping-pong 256x256
+  else if (pl == LAY_RC && ql == LAY_RC) v = (N >= 1536 || R >= 1536) ? 5 : 2;  // forward
+  else v = (N <= 1024 && R <= 1024) ? 1 : 3;                              // dgrad
   (void)M;
   if ((v == 2 || v == 5) && R % 64) v = 1;                                  // BK = 64 configurations need 64-row chunks
   return v;

@@ -4,12 +4,12 @@ Compute runs only in ``lib/libvit_hip.so`` (C-ABI, include/vit_hip.h); this
 package is the host-side mirror of the reference's module/optimizer interface.
 """
 from . import _lib
-from .model import VisionTransformer, create_model, cross_entropy
+from .model import VisionTransformer, create_model, cross_entropy, set_wgrad_overlap
 from .optim import FusedSGD, FusedAdamW, CosineAnnealingLRWithWarmup
 from .dora import DoRALayer, dora_weight
 from . import rsa
 
-__all__ = ["VisionTransformer", "create_model", "cross_entropy", "FusedSGD", "FusedAdamW",
+__all__ = ["VisionTransformer", "create_model", "cross_entropy", "set_wgrad_overlap", "FusedSGD", "FusedAdamW",
            "CosineAnnealingLRWithWarmup", "DoRALayer", "dora_weight", "rsa"]
 
 

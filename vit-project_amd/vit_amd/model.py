@@ -52,6 +52,40 @@ def _put_copy(g: torch.Tensor, copy: torch.Tensor):
     _GRAD_COPY[(g.data_ptr(), g.numel())] = (copy, g._version)
 
 
+# Weight-gradient work of a block's backward runs on a second stream so its
+# MFMA-bound main loops overlap the input-gradient chain's HBM-bound epilogues
+# (GELU', residual and LayerNorm passes).  Fork = side waits on main; the block
+# joins (main waits on side) before returning its gradients.  Capturable.
+_SIDE = {}
+_OVERLAP = [True]
+
+
+def set_wgrad_overlap(enable: bool):
+    """Run weight/bias gradients on a side stream (default) or inline on the caller's stream."""
+    _OVERLAP[0] = bool(enable)
+
+
+class _Side:
+    def __init__(self, dev):
+        self.main = torch.cuda.current_stream(dev)
+        self.on = _OVERLAP[0] and dev.type == "cuda"
+        if self.on:
+            if dev not in _SIDE:
+                _SIDE[dev] = torch.cuda.Stream(device=dev)
+            self.side = _SIDE[dev]
+
+    def run(self, fn):
+        if not self.on:
+            return fn()
+        self.side.wait_stream(self.main)
+        with torch.cuda.stream(self.side):
+            return fn()
+
+    def join(self):
+        if self.on:
+            self.main.wait_stream(self.side)
+
+
 class _Shadowed:
     """Registry of bf16 shadows for GEMM weights."""
 
@@ -169,26 +203,27 @@ class _BlockFn(torch.autograd.Function):
         dxo = dxo.contiguous().reshape(M, D)
         dxo_c = _take_copy(dxo, T)
         gelu_bwd = L.EPI_QGELU_BWD if qg else L.EPI_GELU_BWD
+        side = _Side(dxo.device)
+        # gradient buffers are taken on the main stream (allocator ownership), filled on the side stream
+        g_fc2w, g_fc2b, g_fc1w, g_fc1b = _gout(fc2w), _gout(fc2b), _gout(fc1w), _gout(fc1b)
+        g_projw, g_projb, g_qkvw, g_qkvb = _gout(projw), _gout(projb), _gout(qkvw), _gout(qkvb)
         # MLP
+        d_fc2w, d_fc2b = side.run(lambda: (ops.linear_wgrad(dxo_c, act, out=g_fc2w), ops.colsum(dxo_c, out=g_fc2b)))
         dpre = ops.linear_dgrad(dxo_c, _w(fc2w), out_dtype=T, epi=gelu_bwd, pre=pre)
-        d_fc2w = ops.linear_wgrad(dxo_c, act, out=_gout(fc2w))
-        d_fc2b = ops.colsum(dxo_c, out=_gout(fc2b))
+        d_fc1w, d_fc1b = side.run(lambda: (ops.linear_wgrad(dpre, h2, out=g_fc1w), ops.colsum(dpre, out=g_fc1b)))
         dh2 = ops.linear_dgrad(dpre, _w(fc1w), out_dtype=T)
-        d_fc1w = ops.linear_wgrad(dpre, h2, out=_gout(fc1w))
-        d_fc1b = ops.colsum(dpre, out=_gout(fc1b))
         dxm = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
         dxm_c = dxm if T == torch.float32 else torch.empty(M, D, dtype=T, device=dxo.device)
         d_n2w, d_n2b = _gout(n2w), _gout(n2b)
         ops.layer_norm_bwd(xm, D, dh2, n2w.detach(), m2, r2, dxm, D, M, dres=dxo, ldres=D,
                            dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=d_n2w, dbeta=d_n2b)
         # attention
+        d_projw, d_projb = side.run(lambda: (ops.linear_wgrad(dxm_c, o, out=g_projw),
+                                             ops.colsum(dxm_c, out=g_projb)))
         do = ops.linear_dgrad(dxm_c, _w(projw), out_dtype=T)
-        d_projw = ops.linear_wgrad(dxm_c, o, out=_gout(projw))
-        d_projb = ops.colsum(dxm_c, out=_gout(projb))
         dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N)
+        d_qkvw, d_qkvb = side.run(lambda: (ops.linear_wgrad(dqkv, h1, out=g_qkvw), ops.colsum(dqkv, out=g_qkvb)))
         dh1 = ops.linear_dgrad(dqkv, _w(qkvw), out_dtype=T)
-        d_qkvw = ops.linear_wgrad(dqkv, h1, out=_gout(qkvw))
-        d_qkvb = ops.colsum(dqkv, out=_gout(qkvb))
         dx = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
         d_n1w, d_n1b = _gout(n1w), _gout(n1b)
         if compact_np:
@@ -199,6 +234,7 @@ class _BlockFn(torch.autograd.Function):
                            compact_np=compact_np, dgamma=d_n1w, dbeta=d_n1b)
         if dx_c is not None:
             _put_copy(dx, dx_c)
+        side.join()
         return (dx.reshape(B, N, D), d_n1w, d_n1b, d_qkvw, d_qkvb, d_projw, d_projb, d_n2w, d_n2b, d_fc1w,
                 d_fc1b, d_fc2w, d_fc2b, None)
 
