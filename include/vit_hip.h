@@ -53,9 +53,13 @@ int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const
                    const void* W, const float* bias, void* Y, int64_t ldy, const void* resid,
                    void* act_out, void* stream);
 
-/* F.linear input gradient dX = dY W (+ GELU' epilogue) -- autograd of VIT:142. */
+/* F.linear input gradient dX = dY W (+ GELU' epilogue) -- autograd of VIT:142.  dbias (optional) =
+ * column sums of dX as stored (bias gradient of the Linear that produced dX's forward value, e.g.
+ * fc1.bias from fc2's dgrad), fused into the epilogue; partial >= vit_linear_dgrad_partial_floats. */
 int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, const void* dY, int64_t lddy,
-                     const void* W, void* dX, int64_t lddx, const void* pre, void* stream);
+                     const void* W, void* dX, int64_t lddx, const void* pre, float* dbias, float* partial,
+                     int64_t partial_floats, void* stream);
+int vit_linear_dgrad_partial_floats(int M, int K);
 
 /* F.linear weight gradient dW (f32) = dY^T X, split-K over rows with fp32 slabs
  * in `workspace` (>= split*N*K*4 bytes) -- autograd of VIT:142. */
@@ -65,6 +69,9 @@ int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t ldd
 /* Column sums (bias gradients): out[N] = sum_i X[i][:] -- autograd of VIT:142. */
 int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, float* partial,
                int64_t partial_floats, int accumulate, void* stream);
+/* out[N] (+)= sum_z part[z][:] over S partial rows (second stage of fused bias gradients);
+ * scratch optional (>= ceil(S/64)*N floats, faster for S > 64). */
+int vit_colreduce(const float* part, int S, int N, float* out, int accumulate, float* scratch, void* stream);
 
 /* timm PatchEmbed Conv2d(3,768,16,16) as GEMM over unfolded patches, writing
  * rows b*(np+1)+1+p of the f32 token stream with pos_embed added (VIT:139). */
@@ -82,21 +89,26 @@ int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x,
                        int64_t ldy, const float* w, const float* b, float* mean, float* rstd, float eps,
                        void* stream);
 /* LayerNorm backward with fused residual-gradient add, optional GEMM-dtype copy
- * of dx (optionally dropping CLS rows), dgamma/dbeta. */
+ * of dx (optionally dropping CLS rows), dgamma/dbeta, and dsum = column sums of dx
+ * (bias gradient of the Linear whose output fed the residual: proj / fc2). */
 int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x, int64_t ldx,
                        const void* dy, int64_t lddy, const float* w, const float* mean, const float* rstd,
                        const float* dres, int64_t ldres, float* dx, int64_t lddx, void* dx_copy, int64_t ld_copy,
-                       int dtype_copy, int compact_np, float* dgamma, float* dbeta, float* partial,
+                       int dtype_copy, int compact_np, float* dgamma, float* dbeta, float* dsum, float* partial,
                        int64_t partial_floats, void* stream);
+int vit_layer_norm_bwd_partial_floats(int rows, int D);
 
 /* F.scaled_dot_product_attention(q,k,v) (timm Attention, no mask, head_dim 64,
  * N <= 288) reading q/k/v in place from the qkv GEMM output; lse [B*H*N] f32. */
 int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, void* o,
                  int64_t ld_o, float* lse, float scale, void* stream);
-/* SDPA backward into dqkv (qkv layout). delta_ws >= B*H*N floats (f32 path). */
+/* SDPA backward into dqkv (qkv layout). delta_ws >= B*H*N floats.  dbias (optional, [3*H*64]) =
+ * column sums of dqkv (the qkv Linear's bias gradient), fused into the kernels;
+ * partial >= vit_sdpa_bwd_partial_floats(B, N, H*64). */
 int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, const void* o,
                  int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
-                 float* delta_ws, float scale, void* stream);
+                 float* delta_ws, float scale, float* dbias, float* partial, int64_t partial_floats, void* stream);
+int vit_sdpa_bwd_partial_floats(int B, int N, int D);
 
 /* torch.nn.functional.cross_entropy(outputs, targets) mean (VIT:140) and its gradient. */
 int vit_cross_entropy_fwd(int B, int C, const float* logits, int64_t ld, const int64_t* target, float* row_lse,

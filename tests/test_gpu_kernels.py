@@ -92,8 +92,24 @@ def test_linear_dgrad_and_gelu_bwd():
     pre = _rnd(M, K, seed=10, dtype=torch.bfloat16)
     pf = pre.float().requires_grad_(True)
     torch.nn.functional.gelu(pf).backward(ref)
-    d = ops.linear_dgrad(dy.to(DEV), w.to(DEV), out_dtype=torch.bfloat16, epi=L.EPI_GELU_BWD, pre=pre.to(DEV))
+    db = torch.empty(K, device=DEV)
+    d = ops.linear_dgrad(dy.to(DEV), w.to(DEV), out_dtype=torch.bfloat16, epi=L.EPI_GELU_BWD, pre=pre.to(DEV),
+                         dbias=db)
     _close(d, pf.grad, 8e-3, "gelu bwd")
+    _close(db, pf.grad.sum(0), 1e-3, "fused bias grad (MFMA epilogue)")
+
+
+@pytest.mark.parametrize("M,N,K,dtype", [(197 * 3, 640, 448, torch.bfloat16), (300, 96, 72, torch.float32),
+                                         (70, 64, 40, torch.bfloat16)])
+def test_linear_dgrad_fused_bias(M, N, K, dtype):
+    """dbias = column sums of dX, fused (MFMA path, ragged M) or after the generic kernel."""
+    dy = _rnd(M, N, seed=50, dtype=dtype)
+    w = _rnd(N, K, seed=51, scale=0.05, dtype=dtype)
+    ref = dy.float() @ w.float()
+    db = torch.full((K,), 3.0, device=DEV)
+    dx = ops.linear_dgrad(dy.to(DEV), w.to(DEV), out_dtype=torch.float32, dbias=db)
+    _close(dx, ref, 1e-5, "dgrad")
+    _close(db, ref.sum(0), 1e-5, "dbias")
 
 
 @pytest.mark.parametrize("M,N,K,split", [(1024, 256, 384, 1), (4096, 384, 256, 4), (6336, 256, 128, 7), (6304, 256, 128, 3)])
@@ -209,9 +225,11 @@ def test_layer_norm_fwd_bwd(D, xdt):
     copy = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
     dg = torch.empty(D, device=DEV)
     db = torch.empty(D, device=DEV)
+    ds = torch.empty(D, device=DEV)
     ops.layer_norm_bwd(x.to(DEV), D, dy.to(DEV), w.to(DEV), mean, rstd, dx, D, M, dres=dres.to(DEV), ldres=D,
-                       dx_copy=copy, ld_copy=D, dgamma=dg, dbeta=db)
+                       dx_copy=copy, ld_copy=D, dgamma=dg, dbeta=db, dsum=ds)
     _close(dx, xr.grad + dres, 1e-5, "ln dx")
+    _close(ds, (xr.grad + dres).sum(0), 1e-5, "ln dsum")
     _close(copy, xr.grad + dres, 8e-3, "ln dx copy")
     _close(dg, wr.grad, 1e-5, "dgamma")
     _close(db, br.grad, 1e-5, "dbeta")
@@ -260,8 +278,11 @@ def test_sdpa_fwd_bwd(N, dtype):
     _close(o, o_ref, rel, "o")
     _close(lse, lse_ref, 1e-5 if dtype == torch.float32 else 2e-3, "lse")
     # backward from the reference forward's o so only the bwd kernel is tested
-    dqkv = ops.sdpa_bwd(qkv.to(DEV), o_ref.detach().to(dtype).to(DEV), do.to(DEV), lse_ref.to(DEV), B, H, N)
+    dbias = torch.empty(3 * D, device=DEV)
+    dqkv = ops.sdpa_bwd(qkv.to(DEV), o_ref.detach().to(dtype).to(DEV), do.to(DEV), lse_ref.to(DEV), B, H, N,
+                        dbias=dbias)
     g = dqkv.float().cpu()
+    _close(dbias, torch.cat([dq, dk, dv], 1).sum(0), 1e-4 if dtype == torch.float32 else 3e-2, "qkv bias grad")
     rel = 1e-4 if dtype == torch.float32 else 3e-2
     _close(g[:, :D], dq, rel, "dq")
     _close(g[:, D:2 * D], dk, rel, "dk")

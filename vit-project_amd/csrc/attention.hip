@@ -14,6 +14,10 @@
 // B-operand (k-slot permutation pi), V^T comes from ds_read_b64_tr_b16.
 // f32 path (parity mode): scalar-FMA online softmax.
 #include "common.hpp"
+#include "reduce.hpp"
+
+extern "C" int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, float* partial,
+                          int64_t partial_floats, int accumulate, void* stream);
 
 // 128-B row image with XOR swizzle (row & 6) on 16-B chunks: conflict-free for
 // the 16x16x32 ds_read_b128 fragment reads and for the ds_read_b64_tr_b16 reads
@@ -174,6 +178,40 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
   }
 }
 
+// qkv-bias gradient partials of one (b, h): sum this workgroup's rows of dq (or dk, dv)
+// -- per lane over its rows, across the 16 lanes of a row group, across the 8 waves
+// through LDS (reused after the main loop) -- into out[0..63] (and out[D..] for dk,
+// out[2D..] for dv when NOUT = 2).
+template <int NOUT>
+__device__ __forceinline__ void bias_flush(f32x4 (&c0)[4], f32x4 (*c1)[4], char* smem, float* out, int D) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+  float* red = reinterpret_cast<float*>(smem);  // [NOUT][AT_WAVES][64]
+  __syncthreads();                              // every wave is done reading the LDS images
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) {
+    f32x4 (&c)[4] = o == 0 ? c0 : *c1;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float v = c[dt][t];
+        v += __shfl_xor(v, 1, 64);
+        v += __shfl_xor(v, 2, 64);
+        v += __shfl_xor(v, 4, 64);
+        v += __shfl_xor(v, 8, 64);
+        if ((lane & 15) == 0) red[(o * AT_WAVES + wave) * 64 + dt * 16 + 4 * g + t] = v;
+      }
+  }
+  __syncthreads();
+  if (threadIdx.x < 64 * NOUT) {
+    const int o = threadIdx.x >> 6, d = threadIdx.x & 63;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < AT_WAVES; ++w) sum += red[(o * AT_WAVES + w) * 64 + d];
+    out[(NOUT == 1 ? 0 : (o + 1) * D) + d] = sum;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // bf16 backward, two kernels per (b, h) so each holds only half the head in LDS
 // (57 KiB -> two workgroups per CU):
@@ -188,7 +226,8 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dq(const bf16* __restr
                                                             int N, float scale, const bf16* __restrict__ o,
                                                             int64_t ld_o, const bf16* __restrict__ dout, int64_t ld_do,
                                                             const float* __restrict__ lse, float* __restrict__ delta_out,
-                                                            bf16* __restrict__ dqkv, int64_t ld_dqkv) {
+                                                            bf16* __restrict__ dqkv, int64_t ld_dqkv,
+                                                            float* __restrict__ bias_part) {
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128];
   char* Kimg = smem;
@@ -205,6 +244,9 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dq(const bf16* __restr
   const AtOffsets off(lane);
   __syncthreads();
   const float c2 = scale * LOG2E;
+  f32x4 cs[4];  // column sums of dq (qkv-bias gradient), this lane's rows
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) cs[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   for (int qt = wave; qt < NT; qt += AT_WAVES) {
     const int q = qt * 16 + (lane & 15);
     const int qc = min(q, N - 1);
@@ -256,9 +298,11 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dq(const bf16* __restr
         bf16x4 qv = {(bf16)(dq[dt][0] * scale), (bf16)(dq[dt][1] * scale), (bf16)(dq[dt][2] * scale),
                      (bf16)(dq[dt][3] * scale)};
         *reinterpret_cast<bf16x4*>(row + dt * 16 + 4 * g) = qv;
+        cs[dt] += dq[dt] * scale;
       }
     }
   }
+  if (bias_part) bias_flush<1>(cs, nullptr, smem, bias_part + (int64_t)b * 3 * D + h * 64, D);
 }
 
 template <int NT>
@@ -266,7 +310,7 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
                                                              int N, float scale, const bf16* __restrict__ dout,
                                                              int64_t ld_do, const float* __restrict__ lse,
                                                              const float* __restrict__ delta_in, bf16* __restrict__ dqkv,
-                                                             int64_t ld_dqkv) {
+                                                             int64_t ld_dqkv, float* __restrict__ bias_part) {
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128 + 2 * ROWS * 4];
   char* Qimg = smem;
@@ -290,6 +334,9 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
   const AtOffsets off(lane);
   __syncthreads();
   const float c2 = scale * LOG2E;
+  f32x4 csk[4], csv[4];  // column sums of dk, dv (qkv-bias gradient)
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) { csk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; csv[dt] = csk[dt]; }
   for (int kt = wave; kt < NT; kt += AT_WAVES) {
     const int key = kt * 16 + (lane & 15);
     const bool kvalid = key < N;
@@ -340,9 +387,12 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
         bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
         *reinterpret_cast<bf16x4*>(row + D + dt * 16 + 4 * g) = kv;
         *reinterpret_cast<bf16x4*>(row + 2 * D + dt * 16 + 4 * g) = vv;
+        csk[dt] += dk[dt] * scale;
+        csv[dt] += dv[dt];
       }
     }
   }
+  if (bias_part) bias_flush<2>(csk, &csv, smem, bias_part + (int64_t)b * 3 * D + h * 64, D);
 }
 
 // ---------------------------------------------------------------------------
@@ -539,12 +589,12 @@ static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N,
 template <int NT>
 static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, const void* o,
                     int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, float* delta,
-                    void* dqkv, int64_t ld_dqkv, hipStream_t s) {
+                    void* dqkv, int64_t ld_dqkv, float* bias_part, hipStream_t s) {
   hipLaunchKernelGGL((attn_bwd_dq<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
-                     (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, delta, (bf16*)dqkv, ld_dqkv);
+                     (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, delta, (bf16*)dqkv, ld_dqkv, bias_part);
   VIT_CHECK_LAUNCH();
   hipLaunchKernelGGL((attn_bwd_dkv<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
-                     (const bf16*)dout, ld_do, lse, (const float*)delta, (bf16*)dqkv, ld_dqkv);
+                     (const bf16*)dout, ld_do, lse, (const float*)delta, (bf16*)dqkv, ld_dqkv, bias_part);
   VIT_CHECK_LAUNCH();
   return 0;
 }
@@ -580,20 +630,35 @@ int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
 
 // SDPA backward: writes dq/dk/dv into dqkv (same column layout as qkv).
 // `delta_ws` (>= B*H*N floats) receives rowsum(dO*O) per (b, h, n).
+// dbias (optional, [3D] f32) = column sums of dqkv (the qkv Linear's bias gradient);
+// needs `partial` >= vit_sdpa_bwd_partial_floats(B, N, D) floats.
+int vit_sdpa_bwd_partial_floats(int B, int N, int D) {
+  const int64_t C = 3 * (int64_t)D;
+  const int64_t mfma = B * C + (B > 64 ? (int64_t)((B + 63) / 64) * C : 0);
+  const int64_t gen = 256 * C + 4 * C;  // vit_colsum on the generic path
+  return (int)(mfma > gen ? mfma : gen);
+}
+
 int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, const void* o,
                  int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
-                 float* delta_ws, float scale, void* stream) {
+                 float* delta_ws, float scale, float* dbias, float* partial, int64_t partial_floats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (head_dim != 64 || N <= 0 || N > 288) return (int)hipErrorInvalidValue;
   const int D = H * 64;
   if (!delta_ws) return (int)hipErrorInvalidValue;
+  if (dbias && (partial == nullptr || partial_floats < vit_sdpa_bwd_partial_floats(B, N, D))) return (int)hipErrorInvalidValue;
   if (dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_do % 8 == 0) && (ld_dqkv % 4 == 0) && (ld_o % 4 == 0)) {
     int nt = (N + 15) / 16;
+    int rc = (int)hipErrorInvalidValue;
     switch (nt) {
-#define CASE(n) case n: return bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, s);
+#define CASE(n) case n: rc = bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, dbias ? partial : nullptr, s); break;
       NT_CASES(CASE)
 #undef CASE
     }
+    if (rc || !dbias) return rc;
+    launch_colreduce(partial, B, 3 * D, dbias, 0, s, partial + (int64_t)B * 3 * D);
+    VIT_CHECK_LAUNCH();
+    return 0;
   }
   dim3 grid((N + 63) / 64, B * H);
 #define GEN(T)                                                                                               \
@@ -605,6 +670,7 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
   if (dtype == VIT_BF16) { GEN(bf16) } else { GEN(float) }
 #undef GEN
   VIT_CHECK_LAUNCH();
+  if (dbias) return vit_colsum(dtype, B * N, 3 * D, dqkv, ld_dqkv, dbias, partial, partial_floats, 0, stream);
   return 0;
 }
 

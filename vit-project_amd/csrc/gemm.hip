@@ -34,6 +34,7 @@ struct Epi {
   const float* pos;         // EPI_PATCH: pos_embed [seq, N]
   int n_patch;              // EPI_PATCH: patches per image (seq = n_patch + 1)
   int64_t slab;             // split-r: element offset of slab z
+  float* csum;              // optional column sums of the epilogue output: [ceil(M/64)][N] partials (64-row groups)
   int dbg;                  // timing experiments only (vit_gemm_variant(v + 100*bits)): 1 = no in-loop loads, 2 = no in-loop barriers, 4 = no epilogue
 };
 
@@ -56,16 +57,18 @@ template <> __device__ __forceinline__ f32x4 load4<bf16>(const bf16* p) {
 
 // Apply the epilogue to 4 consecutive output columns j..j+3 of row i.
 template <int EPI, typename TO, typename TA>
-__device__ __forceinline__ void epi4(const Epi& e, int i, int j, f32x4 v, int z = 0) {
+__device__ __forceinline__ f32x4 epi4(const Epi& e, int i, int j, f32x4 v, int z = 0) {
   if (e.bias) {
     f32x4 b = *reinterpret_cast<const f32x4*>(e.bias + j);
     v += b;
   }
   if constexpr (EPI == EPI_STORE) {
     store4<TO>((TO*)e.C + e.slab * z + (int64_t)i * e.ldc + j, v);
+    return v;
   } else if constexpr (EPI == EPI_ACC) {
     TO* c = (TO*)e.C + (int64_t)i * e.ldc + j;
     store4<TO>(c, v + load4<TO>(c));
+    return v;
   } else if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) {
     // the activation is computed from the rounded pre-activation that backward sees
     store4<TO>((TO*)e.C + (int64_t)i * e.ldc + j, v);
@@ -76,9 +79,11 @@ __device__ __forceinline__ void epi4(const Epi& e, int i, int j, f32x4 v, int z 
 #pragma unroll
     for (int t = 0; t < 4; ++t) a[t] = (EPI == EPI_BIAS_GELU) ? gelu_fast(pre_r[t]) : quick_gelu(pre_r[t]);
     store4<TO>((TO*)e.aux_out + (int64_t)i * e.ldc + j, a);
+    return v;
   } else if constexpr (EPI == EPI_RESID) {
     f32x4 r = load4<float>((const float*)e.aux + (int64_t)i * e.ld_aux + j);
     store4<TO>((TO*)e.C + (int64_t)i * e.ldc + j, v + r);
+    return v;
   } else if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
     f32x4 pre = load4<TA>((const TA*)e.aux + (int64_t)i * e.ld_aux + j);
 #pragma unroll
@@ -89,6 +94,32 @@ __device__ __forceinline__ void epi4(const Epi& e, int i, int j, f32x4 v, int z 
     int64_t row = (int64_t)b * (e.n_patch + 1) + 1 + p;
     f32x4 ps = *reinterpret_cast<const f32x4*>(e.pos + (int64_t)(1 + p) * e.ldc + j);
     store4<TO>((TO*)e.C + row * e.ldc + j, v + ps);
+    return v;
+  }
+  return v;
+}
+
+
+// Column sums of a wave's epilogue outputs over one 64-row group (4 accumulator
+// rows of 16): cs[b] holds this lane's partial for columns j..j+3 of fragment b;
+// reduce over the 16 lanes of each row group and store one partial row.
+template <int AJ>
+__device__ __forceinline__ void csum_flush(const Epi& e, f32x4 (&cs)[AJ], int row0, int M, int N, int jbase, int lane) {
+#pragma unroll
+  for (int b = 0; b < AJ; ++b) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float v = cs[b][t];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      cs[b][t] = v;
+    }
+    const int j = jbase + b * 16 + 4 * (lane >> 4);
+    if ((lane & 15) == 0 && row0 < M && j < N)
+      *reinterpret_cast<f32x4*>(e.csum + (int64_t)(row0 >> 6) * N + j) = cs[b];
+    cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
 }
 
@@ -141,6 +172,7 @@ template <int BM_, int BN_, int BK_, int WI_, int WJ_, int S_, bool DB_, int OCC
   static constexpr int G = GP + GQ;  // global_load_lds per wave per stage
   static constexpr int LDS = STAGES * STAGE;
   static_assert(GP * 1024 * WAVES == PIMG && GQ * 1024 * WAVES == QIMG, "stage must split into 1-KiB pieces per wave");
+  static_assert(AI % 4 == 0, "column-sum epilogue works on 64-row groups");
   static_assert(LDS <= 163840, "LDS");
 };
 
@@ -369,14 +401,21 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
     return;
   }
   // epilogue: acc[a][b] holds C[i][j..j+3] with i = lane&15, j = 4*(lane>>4)
+  f32x4 cs[C::AJ];
+#pragma unroll
+  for (int b = 0; b < C::AJ; ++b) cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int a = 0; a < C::AI; ++a) {
     const int i = i0 + wi * C::WM + a * 16 + (lane & 15);
 #pragma unroll
     for (int b = 0; b < C::AJ; ++b) {
       const int j = j0 + wj * C::WN + b * 16 + 4 * (lane >> 4);
-      if (i < M && j < N) epi4<EPI, TO, TA>(e, i, j, acc[a][b], z);
+      if (i < M && j < N) {
+        const f32x4 v = epi4<EPI, TO, TA>(e, i, j, acc[a][b], z);
+        if (e.csum) cs[b] += v;
+      }
     }
+    if (e.csum && (a & 3) == 3) csum_flush<C::AJ>(e, cs, i0 + wi * C::WM + (a - 3) * 16, M, N, j0 + wj * C::WN, lane);
   }
 }
 
@@ -542,14 +581,21 @@ __global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, 
       for (int b = 0; b < 4; ++b) asm volatile("" ::"v"(acc[a][b]));
     return;
   }
+  f32x4 cs[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     const int i = i0 + grp * 128 + a * 16 + (lane & 15);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const int j = j0 + wj * 64 + b * 16 + 4 * (lane >> 4);
-      if (i < M && j < N) epi4<EPI, TO, TA>(e, i, j, acc[a][b], z);
+      if (i < M && j < N) {
+        const f32x4 v = epi4<EPI, TO, TA>(e, i, j, acc[a][b], z);
+        if (e.csum) cs[b] += v;
+      }
     }
+    if (e.csum && (a & 3) == 3) csum_flush<4>(e, cs, i0 + grp * 128 + (a - 3) * 16, M, N, j0 + wj * 64, lane);
   }
 }
 
@@ -832,12 +878,50 @@ int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const
   return gemm_any(epi, dtype, out_dtype, LAY_RC, LAY_RC, M, N, K, X, ldx, W, K, 1, e, (hipStream_t)stream);
 }
 
-// Linear input gradient: dX[M,K] = dY[M,N] W[N,K]  (epi EPI_STORE or *_GELU_BWD with pre [M,K])
+// Linear input gradient: dX[M,K] = dY[M,N] W[N,K]  (epi EPI_STORE or *_GELU_BWD with pre [M,K]).
+// dbias (optional, [K] f32) = column sums of dX as written by the epilogue (the bias
+// gradient of the Linear whose output gradient dX is, e.g. fc1's from fc2's dgrad with
+// the GELU' epilogue); needs `partial` >= vit_linear_dgrad_partial_floats(M, K).
+int vit_linear_dgrad_partial_floats(int M, int K) {
+  const int rows = (M + 63) / 64;
+  return (int)((int64_t)rows * K + colreduce_scratch_floats(rows, K));
+}
+
 int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, const void* dY, int64_t lddy,
-                     const void* W, void* dX, int64_t lddx, const void* pre, void* stream) {
+                     const void* W, void* dX, int64_t lddx, const void* pre, float* dbias, float* partial,
+                     int64_t partial_floats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
   Epi e = make_epi();
   e.C = dX; e.ldc = lddx; e.aux = pre; e.ld_aux = lddx;
-  return gemm_any(epi, dtype, out_dtype, LAY_RC, LAY_CR, M, K, N, dY, lddy, W, K, 1, e, (hipStream_t)stream);
+  const int rows = (M + 63) / 64;
+  const bool fast = fast_ok(dtype, M, K, N, dY, W, lddy, K) && (lddx % 4 == 0);
+  if (dbias) {
+    if (partial == nullptr || partial_floats < vit_linear_dgrad_partial_floats(M, K)) return (int)hipErrorInvalidValue;
+    if (fast) e.csum = partial;
+  }
+  int rc = gemm_any(epi, dtype, out_dtype, LAY_RC, LAY_CR, M, K, N, dY, lddy, W, K, 1, e, s);
+  if (rc || !dbias || M <= 0) return rc;
+  if (!fast) {  // generic path: column sums of the stored output
+    if (out_dtype == VIT_BF16)
+      hipLaunchKernelGGL(colsum_partial_kernel<bf16>, dim3((K + 255) / 256, rows), dim3(256), 0, s, (const bf16*)dX,
+                         lddx, M, K, 64, partial);
+    else
+      hipLaunchKernelGGL(colsum_partial_kernel<float>, dim3((K + 255) / 256, rows), dim3(256), 0, s, (const float*)dX,
+                         lddx, M, K, 64, partial);
+    VIT_CHECK_LAUNCH();
+  }
+  launch_colreduce(partial, rows, K, dbias, 0, s, partial + (int64_t)rows * K);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+// Column reduction out[N] (+)= sum_z part[z][N] (second stage of fused bias gradients);
+// scratch (optional) >= ceil(S/64)*N floats.
+int vit_colreduce(const float* part, int S, int N, float* out, int accumulate, float* scratch, void* stream) {
+  if (S <= 0 || N <= 0) return 0;
+  launch_colreduce(part, S, N, out, accumulate, (hipStream_t)stream, scratch);
+  VIT_CHECK_LAUNCH();
+  return 0;
 }
 
 // Linear weight gradient: dW[N,K] (f32) = dY[M,N]^T X[M,K], split over M into
@@ -894,7 +978,8 @@ int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, f
   else
     hipLaunchKernelGGL(colsum_partial_kernel<float>, g1, dim3(256), 0, s, (const float*)X, ld, M, N, rows_per, partial);
   VIT_CHECK_LAUNCH();
-  launch_colreduce(partial, S, N, out, accumulate, s);
+  float* scratch = partial_floats >= (int64_t)S * N + colreduce_scratch_floats(S, N) ? partial + (int64_t)S * N : nullptr;
+  launch_colreduce(partial, S, N, out, accumulate, s, scratch);
   VIT_CHECK_LAUNCH();
   return 0;
 }

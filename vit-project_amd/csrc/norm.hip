@@ -88,13 +88,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     const float* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
     const float* __restrict__ dres, int64_t ldres, float* __restrict__ dx, int64_t lddx,
     TC* __restrict__ dxc, int64_t ldc, int compact_np, float* __restrict__ part_g,
-    float* __restrict__ part_b, int rows, int D, int rows_per) {
+    float* __restrict__ part_b, float* __restrict__ part_s, int rows, int D, int rows_per) {
   constexpr int NP = NV > 0 ? NV * 4 : LN_SMAX;  // partial slots per lane
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  float pg[NP], pb[NP];
+  float pg[NP], pb[NP], ps[NP];
 #pragma unroll
-  for (int t = 0; t < NP; ++t) { pg[t] = 0.f; pb[t] = 0.f; }
-  __shared__ float red[LN_WAVES][128];
+  for (int t = 0; t < NP; ++t) { pg[t] = 0.f; pb[t] = 0.f; ps[t] = 0.f; }
+  __shared__ float red[LN_WAVES][192];
   const int r0 = blockIdx.x * rows_per, r1 = min(rows, r0 + rows_per);
   for (int row = r0 + wv; row < r1; row += LN_WAVES) {
     const TX* xr = x + (int64_t)row * ldx;
@@ -129,6 +129,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 #pragma unroll
         for (int t = 0; t < 4; ++t) o[t] = rs * (g[k][t] - s1 - xh[k][t] * s2);
         if (dres) o += *reinterpret_cast<const f32x4*>(dres + (int64_t)row * ldres + c);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) ps[k * 4 + t] += o[t];
         *reinterpret_cast<f32x4*>(dxr + c) = o;
         if (keep) st4<TC>(dxc + orow * ldc + c, o);
       }
@@ -145,28 +147,35 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
       }
       s1 = wave_sum(s1) / D;
       s2 = wave_sum(s2) / D;
-      for (int c = lane; c < D; c += 64) {
+#pragma unroll
+      for (int k = 0; k < LN_SMAX; ++k) {
+        const int c = lane + 64 * k;
+        if (c >= D) break;
         float xh = ((float)xr[c] - mu) * rs, g = (float)dyr[c] * w[c];
         float o = rs * (g - s1 - xh * s2);
         if (dres) o += dres[(int64_t)row * ldres + c];
+        ps[k] += o;
         dxr[c] = o;
         if (keep) dxc[orow * ldc + c] = (TC)o;
       }
     }
   }
-  if (!part_g) return;
-  float* out_g = part_g + (int64_t)blockIdx.x * D;
-  float* out_b = part_b + (int64_t)blockIdx.x * D;
+  if (!part_g && !part_s) return;
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     const int c = NV > 0 ? col4(lane, k >> 2) + (k & 3) : k * 64 + lane;
     if (NV == 0 && k * 64 >= D) break;  // uniform across the block
     red[wv][lane] = pg[k];
     red[wv][64 + lane] = pb[k];
+    red[wv][128 + lane] = ps[k];
     __syncthreads();
     if (wv == 0 && c < D) {
-      out_g[c] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-      out_b[c] = (red[0][64 + lane] + red[1][64 + lane]) + (red[2][64 + lane] + red[3][64 + lane]);
+      const int64_t o = (int64_t)blockIdx.x * D + c;
+      if (part_g) {
+        part_g[o] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+        part_b[o] = (red[0][64 + lane] + red[1][64 + lane]) + (red[2][64 + lane] + red[3][64 + lane]);
+      }
+      if (part_s) part_s[o] = (red[0][128 + lane] + red[1][128 + lane]) + (red[2][128 + lane] + red[3][128 + lane]);
     }
     __syncthreads();
   }
@@ -193,9 +202,9 @@ template <typename TX, typename TD, typename TC>
 static void launch_bwd(int nv, int nblk, hipStream_t s, const void* x, int64_t ldx, const void* dy, int64_t lddy,
                        const float* w, const float* mean, const float* rstd, const float* dres, int64_t ldres,
                        float* dx, int64_t lddx, void* dxc, int64_t ldc, int compact_np, float* pg, float* pb,
-                       int rows, int D, int rows_per) {
+                       float* ps, int rows, int D, int rows_per) {
 #define B(NV) hipLaunchKernelGGL((ln_bwd_kernel<NV, TX, TD, TC>), dim3(nblk), dim3(64 * LN_WAVES), 0, s, (const TX*)x, ldx, \
-                                 (const TD*)dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, (TC*)dxc, ldc, compact_np, pg, pb, rows, D, rows_per)
+                                 (const TD*)dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, (TC*)dxc, ldc, compact_np, pg, pb, ps, rows, D, rows_per)
   switch (nv) {
     case 3: B(3); break;
     case 4: B(4); break;
@@ -227,32 +236,37 @@ int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x,
 // LayerNorm backward.  dx (f32) = dres + LN'(dy).  dx_copy (optional, dtype_copy,
 // row stride ld_copy) is the GEMM-operand copy of dx; compact_np > 0 drops the
 // CLS row of every (compact_np+1)-row image (patch-embed wgrad operand).
-// dgamma/dbeta (may be null) need `partial` >= 2*nblk*D floats, nblk = ceil(rows/rows_per).
+// dgamma/dbeta and dsum = column sums of dx (the bias gradient of the Linear that
+// produced the LayerNorm's residual input) may each be null; `partial` must hold
+// vit_layer_norm_bwd_partial_floats(rows, D) floats when any of them is requested.
+int vit_layer_norm_bwd_partial_floats(int rows, int D) {
+  const int nblk = (rows + 63) / 64;
+  return (int)(3 * (int64_t)nblk * D + colreduce_scratch_floats(nblk, D));
+}
+
 int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x, int64_t ldx,
                        const void* dy, int64_t lddy, const float* w, const float* mean, const float* rstd,
                        const float* dres, int64_t ldres, float* dx, int64_t lddx, void* dx_copy, int64_t ld_copy,
-                       int dtype_copy, int compact_np, float* dgamma, float* dbeta, float* partial,
+                       int dtype_copy, int compact_np, float* dgamma, float* dbeta, float* dsum, float* partial,
                        int64_t partial_floats, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (rows <= 0) return 0;
   if (D > 64 * LN_SMAX) return (int)hipErrorInvalidValue;
-  int rows_per = 64;
-  int nblk = (rows + rows_per - 1) / rows_per;
-  if (dgamma) {
-    while ((int64_t)2 * nblk * D > partial_floats && rows_per < rows) {
-      rows_per *= 2;
-      nblk = (rows + rows_per - 1) / rows_per;
-    }
-    if ((int64_t)2 * nblk * D > partial_floats) return (int)hipErrorInvalidValue;
-  }
+  const int rows_per = 64;
+  const int nblk = (rows + rows_per - 1) / rows_per;
+  const bool want = dgamma != nullptr || dsum != nullptr;
+  if (want && (partial == nullptr || partial_floats < vit_layer_norm_bwd_partial_floats(rows, D)))
+    return (int)hipErrorInvalidValue;
   float* pg = dgamma ? partial : nullptr;
   float* pb = dgamma ? partial + (int64_t)nblk * D : nullptr;
+  float* ps = dsum ? partial + 2 * (int64_t)nblk * D : nullptr;
+  float* scratch = want ? partial + 3 * (int64_t)nblk * D : nullptr;
   bool vec = (D % 256 == 0) && (ldx % 4 == 0) && (lddy % 4 == 0) && (lddx % 4 == 0) && (ldres % 4 == 0) &&
              (ld_copy % 4 == 0);
   int nv = vec ? D / 256 : 0;
 #define LB(TX, TD) \
-  if (dtype_copy == VIT_BF16) launch_bwd<TX, TD, bf16>(nv, nblk, s, x, ldx, dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, dx_copy, ld_copy, compact_np, pg, pb, rows, D, rows_per); \
-  else launch_bwd<TX, TD, float>(nv, nblk, s, x, ldx, dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, dx_copy, ld_copy, compact_np, pg, pb, rows, D, rows_per);
+  if (dtype_copy == VIT_BF16) launch_bwd<TX, TD, bf16>(nv, nblk, s, x, ldx, dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, dx_copy, ld_copy, compact_np, pg, pb, ps, rows, D, rows_per); \
+  else launch_bwd<TX, TD, float>(nv, nblk, s, x, ldx, dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, dx_copy, ld_copy, compact_np, pg, pb, ps, rows, D, rows_per);
   if (dtype_x == VIT_F32 && dtype_dy == VIT_F32) { LB(float, float) }
   else if (dtype_x == VIT_F32) { LB(float, bf16) }
   else if (dtype_dy == VIT_BF16) { LB(bf16, bf16) }
@@ -260,11 +274,11 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
 #undef LB
   VIT_CHECK_LAUNCH();
   if (dgamma) {
-    launch_colreduce(pg, nblk, D, dgamma, 0, s);
-    VIT_CHECK_LAUNCH();
-    launch_colreduce(pb, nblk, D, dbeta, 0, s);
-    VIT_CHECK_LAUNCH();
+    launch_colreduce(pg, nblk, D, dgamma, 0, s, scratch);
+    launch_colreduce(pb, nblk, D, dbeta, 0, s, scratch);
   }
+  if (dsum) launch_colreduce(ps, nblk, D, dsum, 0, s, scratch);
+  VIT_CHECK_LAUNCH();
   return 0;
 }
 

@@ -36,20 +36,25 @@ from . import ops
 _GRAD_COPY = {}
 
 
-def _take_copy(g: torch.Tensor, dtype):
+def _take_copy(g: torch.Tensor, dtype, want_dsum: bool = False):
+    """The GEMM-dtype copy of an incoming gradient (written by the producer's LayerNorm
+    backward) and, with want_dsum, its column sums (None if the producer did not make them)."""
     key = (g.data_ptr(), g.numel())
     c = _GRAD_COPY.pop(key, None)
-    if c is not None and c[1] == g._version and c[0].dtype == dtype:
-        return c[0]
-    if dtype == torch.float32:
-        return g
-    out = torch.empty(g.shape, dtype=dtype, device=g.device)
-    ops.cast_bf16(g.contiguous(), out)
-    return out
+    fresh = c is not None and c[1] == g._version
+    dsum = c[2] if fresh else None
+    if fresh and c[0] is not None and c[0].dtype == dtype:
+        out = c[0]
+    elif dtype == torch.float32:
+        out = g
+    else:
+        out = torch.empty(g.shape, dtype=dtype, device=g.device)
+        ops.cast_bf16(g.contiguous(), out)
+    return (out, dsum) if want_dsum else out
 
 
-def _put_copy(g: torch.Tensor, copy: torch.Tensor):
-    _GRAD_COPY[(g.data_ptr(), g.numel())] = (copy, g._version)
+def _put_copy(g: torch.Tensor, copy, dsum=None):
+    _GRAD_COPY[(g.data_ptr(), g.numel())] = (copy, g._version, dsum)
 
 
 # Weight-gradient work of a block's backward runs on a second stream so its
@@ -181,14 +186,41 @@ class _BlockFn(torch.autograd.Function):
         H, T, eps = cfg["heads"], cfg["dtype"], cfg["eps"]
         act_epi = L.EPI_BIAS_QGELU if cfg["quick_gelu"] else L.EPI_BIAS_GELU
         M = B * N
+        dev = x.device
         x2 = x.reshape(M, D)
-        h1, m1, r1 = ops.layer_norm_fwd(x2, n1w.detach(), n1b.detach(), eps, T)
-        qkv = ops.linear_fwd(h1, _w(qkvw), qkvb.detach())
-        o, lse = ops.sdpa_fwd(qkv, B, H, N)
-        xm = ops.linear_fwd(o, _w(projw), projb.detach(), epi=L.EPI_RESID, resid=x2)
-        h2, m2, r2 = ops.layer_norm_fwd(xm, n2w.detach(), n2b.detach(), eps, T)
-        pre, act = ops.linear_fwd(h2, _w(fc1w), fc1b.detach(), epi=act_epi)
-        xo = ops.linear_fwd(act, _w(fc2w), fc2b.detach(), epi=L.EPI_RESID, resid=xm)
+        F = fc1w.shape[0]
+        f32 = torch.float32
+        h1, h2 = torch.empty(M, D, dtype=T, device=dev), torch.empty(M, D, dtype=T, device=dev)
+        m1, r1, m2, r2 = (torch.empty(M, dtype=f32, device=dev) for _ in range(4))
+        qkv = torch.empty(M, 3 * D, dtype=T, device=dev)
+        o = torch.empty(M, D, dtype=T, device=dev)
+        lse = torch.empty(B * H * N, dtype=f32, device=dev)
+        xm, xo = torch.empty(M, D, dtype=f32, device=dev), torch.empty(M, D, dtype=f32, device=dev)
+        pre, act = torch.empty(M, F, dtype=T, device=dev), torch.empty(M, F, dtype=T, device=dev)
+        Wqkv, Wproj, W1, W2 = _w(qkvw), _w(projw), _w(fc1w), _w(fc2w)
+
+        def chain(b0, b1):
+            """The block over images [b0, b1): rows b0*N .. b1*N of every tensor."""
+            r0, r1_ = b0 * N, b1 * N
+            sl = slice(r0, r1_)
+            ops.layer_norm_fwd(x2[sl], n1w.detach(), n1b.detach(), eps, T, out=h1[sl], mean=m1[sl], rstd=r1[sl])
+            ops.linear_fwd(h1[sl], Wqkv, qkvb.detach(), out=qkv[sl])
+            ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N])
+            ops.linear_fwd(o[sl], Wproj, projb.detach(), epi=L.EPI_RESID, resid=x2[sl], out=xm[sl])
+            ops.layer_norm_fwd(xm[sl], n2w.detach(), n2b.detach(), eps, T, out=h2[sl], mean=m2[sl], rstd=r2[sl])
+            ops.linear_fwd(h2[sl], W1, fc1b.detach(), epi=act_epi, out=pre[sl], act_out=act[sl])
+            ops.linear_fwd(act[sl], W2, fc2b.detach(), epi=L.EPI_RESID, resid=xm[sl], out=xo[sl])
+
+        side = _Side(dev)
+        if side.on and B >= 2 and T != torch.float32:
+            # two half-batch chains on two streams: one chain's GEMM epilogues (HBM-bound)
+            # overlap the other's MFMA main loops
+            hb = B // 2
+            side.run(lambda: chain(hb, B))
+            chain(0, hb)
+            side.join()
+        else:
+            chain(0, B)
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, pre, act)
         ctx.params = (n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.meta = (B, N, D, H, T, cfg.get("compact_np", 0), cfg["quick_gelu"])
@@ -201,28 +233,37 @@ class _BlockFn(torch.autograd.Function):
         B, N, D, H, T, compact_np, qg = ctx.meta
         M = B * N
         dxo = dxo.contiguous().reshape(M, D)
-        dxo_c = _take_copy(dxo, T)
+        dxo_c, dxo_sum = _take_copy(dxo, T, want_dsum=True)
         gelu_bwd = L.EPI_QGELU_BWD if qg else L.EPI_GELU_BWD
         side = _Side(dxo.device)
         # gradient buffers are taken on the main stream (allocator ownership), filled on the side stream
         g_fc2w, g_fc2b, g_fc1w, g_fc1b = _gout(fc2w), _gout(fc2b), _gout(fc1w), _gout(fc1b)
         g_projw, g_projb, g_qkvw, g_qkvb = _gout(projw), _gout(projb), _gout(qkvw), _gout(qkvb)
-        # MLP
-        d_fc2w, d_fc2b = side.run(lambda: (ops.linear_wgrad(dxo_c, act, out=g_fc2w), ops.colsum(dxo_c, out=g_fc2b)))
-        dpre = ops.linear_dgrad(dxo_c, _w(fc2w), out_dtype=T, epi=gelu_bwd, pre=pre)
-        d_fc1w, d_fc1b = side.run(lambda: (ops.linear_wgrad(dpre, h2, out=g_fc1w), ops.colsum(dpre, out=g_fc1b)))
+        # MLP.  Bias gradients are column sums fused into the kernels that produce each
+        # gradient: fc2.bias from the upstream LayerNorm backward (side channel), fc1.bias
+        # from the GELU' dgrad epilogue, proj.bias from LN2 backward, qkv.bias from SDPA backward.
+        if dxo_sum is not None:
+            d_fc2b = ops.colreduce(dxo_sum, 1, D, g_fc2b)
+        else:
+            d_fc2b = ops.colsum(dxo_c, out=g_fc2b)
+        d_fc2w = side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g_fc2w))
+        dpre = ops.linear_dgrad(dxo_c, _w(fc2w), out_dtype=T, epi=gelu_bwd, pre=pre, dbias=g_fc1b)
+        d_fc1b = g_fc1b
+        d_fc1w = side.run(lambda: ops.linear_wgrad(dpre, h2, out=g_fc1w))
         dh2 = ops.linear_dgrad(dpre, _w(fc1w), out_dtype=T)
         dxm = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
         dxm_c = dxm if T == torch.float32 else torch.empty(M, D, dtype=T, device=dxo.device)
         d_n2w, d_n2b = _gout(n2w), _gout(n2b)
         ops.layer_norm_bwd(xm, D, dh2, n2w.detach(), m2, r2, dxm, D, M, dres=dxo, ldres=D,
-                           dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=d_n2w, dbeta=d_n2b)
+                           dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=d_n2w, dbeta=d_n2b,
+                           dsum=g_projb)
+        d_projb = g_projb
         # attention
-        d_projw, d_projb = side.run(lambda: (ops.linear_wgrad(dxm_c, o, out=g_projw),
-                                             ops.colsum(dxm_c, out=g_projb)))
+        d_projw = side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g_projw))
         do = ops.linear_dgrad(dxm_c, _w(projw), out_dtype=T)
-        dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N)
-        d_qkvw, d_qkvb = side.run(lambda: (ops.linear_wgrad(dqkv, h1, out=g_qkvw), ops.colsum(dqkv, out=g_qkvb)))
+        dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g_qkvb)
+        d_qkvb = g_qkvb
+        d_qkvw = side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g_qkvw))
         dh1 = ops.linear_dgrad(dqkv, _w(qkvw), out_dtype=T)
         dx = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
         d_n1w, d_n1b = _gout(n1w), _gout(n1b)
@@ -230,10 +271,12 @@ class _BlockFn(torch.autograd.Function):
             dx_c = torch.empty(B * compact_np, D, dtype=T, device=dxo.device)
         else:
             dx_c = None if T == torch.float32 else torch.empty(M, D, dtype=T, device=dxo.device)
+        # column sums of dx = the upstream block's fc2.bias gradient (not needed below the first block)
+        dsum = None if compact_np else torch.empty(D, dtype=torch.float32, device=dxo.device)
         ops.layer_norm_bwd(x2, D, dh1, n1w.detach(), m1, r1, dx, D, M, dres=dxm, ldres=D, dx_copy=dx_c, ld_copy=D,
-                           compact_np=compact_np, dgamma=d_n1w, dbeta=d_n1b)
-        if dx_c is not None:
-            _put_copy(dx, dx_c)
+                           compact_np=compact_np, dgamma=d_n1w, dbeta=d_n1b, dsum=dsum)
+        if dx_c is not None or dsum is not None:
+            _put_copy(dx, dx_c, dsum)
         side.join()
         return (dx.reshape(B, N, D), d_n1w, d_n1b, d_qkvw, d_qkvb, d_projw, d_projb, d_n2w, d_n2b, d_fc1w,
                 d_fc1b, d_fc2w, d_fc2b, None)
@@ -266,10 +309,10 @@ class _HeadFn(torch.autograd.Function):
         if T != torch.float32:
             dx_c = ops.zero_(torch.empty(B * N, D, dtype=T, device=x.device))
         dnw, dnb = _gout(nw), _gout(nb)
+        dsum = torch.empty(D, dtype=torch.float32, device=x.device)  # last block's fc2.bias gradient
         ops.layer_norm_bwd(x, N * D, dxc, nw.detach(), mc, rc, dx, N * D, B, dx_copy=dx_c, ld_copy=N * D,
-                           dgamma=dnw, dbeta=dnb)
-        if dx_c is not None:
-            _put_copy(dx, dx_c)
+                           dgamma=dnw, dbeta=dnb, dsum=dsum)
+        _put_copy(dx, dx_c, dsum)
         return dx, dnw, dnb, dhw, dhb, None
 
 

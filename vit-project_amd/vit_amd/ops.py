@@ -63,8 +63,9 @@ def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, res
     return (out, act_out) if epi in (L.EPI_BIAS_GELU, L.EPI_BIAS_QGELU) else out
 
 
-def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, out=None):
-    """dx = dy @ w  (dy [M,N], w [N,K]) with optional activation-grad epilogue on pre [M,K]."""
+def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, out=None, dbias=None):
+    """dx = dy @ w  (dy [M,N], w [N,K]) with optional activation-grad epilogue on pre [M,K];
+    dbias [K] (optional) receives the column sums of dx (fused into the GEMM epilogue)."""
     M, N = dy2d.shape
     K = w.shape[1]
     assert w.shape[0] == N and w.dtype == dy2d.dtype and dy2d.stride(1) == 1
@@ -72,8 +73,19 @@ def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, ou
         out = torch.empty(M, K, dtype=out_dtype, device=dy2d.device)
     if pre is not None:
         assert pre.stride(0) == out.stride(0)
+    part, nfl = None, 0
+    if dbias is not None:
+        assert dbias.dtype == torch.float32 and dbias.is_contiguous() and dbias.numel() == K
+        nfl = L.lib().vit_linear_dgrad_partial_floats(M, K)
+        part = workspace("dgrad_bias", nfl * 4, dy2d.device)
     call("vit_linear_dgrad", L.dt(dy2d), L.dt(out), epi, M, N, K, ptr(dy2d), dy2d.stride(0), ptr(w), ptr(out),
-         out.stride(0), ptr(pre), _s(dy2d))
+         out.stride(0), ptr(pre), ptr(dbias), ptr(part), nfl, _s(dy2d))
+    return out
+
+
+def colreduce(part, S, N, out, accumulate=False, scratch=None):
+    """out[N] (+)= part[:S].sum(0) (partials from a fused epilogue)."""
+    call("vit_colreduce", ptr(part), S, N, ptr(out), int(accumulate), ptr(scratch), _s(out))
     return out
 
 
@@ -106,8 +118,9 @@ def colsum(x2d, out=None, accumulate=False):
     if out is None:
         out = torch.empty(N, dtype=torch.float32, device=x2d.device)
     S = max(1, min(256, M // 64))
-    part = workspace("colsum", S * N * 4, x2d.device)
-    call("vit_colsum", L.dt(x2d), M, N, ptr(x2d), x2d.stride(0), ptr(out), ptr(part), S * N, int(accumulate),
+    nfl = (S + (S + 63) // 64) * N
+    part = workspace("colsum", nfl * 4, x2d.device)
+    call("vit_colsum", L.dt(x2d), M, N, ptr(x2d), x2d.stride(0), ptr(out), ptr(part), nfl, int(accumulate),
          _s(x2d))
     return out
 
@@ -116,14 +129,13 @@ def colsum(x2d, out=None, accumulate=False):
 # LayerNorm
 # ----------------------------------------------------------------------------
 
-def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, need_stats=True):
+def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, need_stats=True, mean=None, rstd=None):
     rows = x2d.shape[0] if rows is None else rows
     D = w.numel()
     ldx = x2d.stride(0) if ldx is None else ldx
     if out is None:
         out = torch.empty(rows, D, dtype=out_dtype, device=x2d.device)
-    mean = rstd = None
-    if need_stats:
+    if need_stats and mean is None:
         mean = torch.empty(rows, dtype=torch.float32, device=x2d.device)
         rstd = torch.empty(rows, dtype=torch.float32, device=x2d.device)
     call("vit_layer_norm_fwd", L.dt(x2d), L.dt(out), rows, D, ptr(x2d), ldx, ptr(out), out.stride(0), ptr(w),
@@ -132,42 +144,49 @@ def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, nee
 
 
 def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0, dx_copy=None, ld_copy=0,
-                   compact_np=0, dgamma=None, dbeta=None):
+                   compact_np=0, dgamma=None, dbeta=None, dsum=None, ws="ln_partial"):
+    """dsum [D] (optional) receives the column sums of dx (a Linear bias gradient)."""
     D = w.numel()
     part = None
     nfl = 0
-    if dgamma is not None:
-        nblk = (rows + 63) // 64
-        nfl = 2 * nblk * D
-        part = workspace("ln_partial", nfl * 4, x.device)
+    if dgamma is not None or dsum is not None:
+        nfl = L.lib().vit_layer_norm_bwd_partial_floats(rows, D)
+        part = workspace(ws, nfl * 4, x.device)
     call("vit_layer_norm_bwd", L.dt(x), L.dt(dy), rows, D, ptr(x), ldx, ptr(dy), dy.stride(0), ptr(w), ptr(mean),
          ptr(rstd), ptr(dres), ldres, ptr(dx), lddx, ptr(dx_copy), ld_copy,
-         L.dt(dx_copy) if dx_copy is not None else L.BF16, compact_np, ptr(dgamma), ptr(dbeta), ptr(part), nfl,
-         _s(x))
+         L.dt(dx_copy) if dx_copy is not None else L.BF16, compact_np, ptr(dgamma), ptr(dbeta), ptr(dsum), ptr(part),
+         nfl, _s(x))
 
 
 # ----------------------------------------------------------------------------
 # attention
 # ----------------------------------------------------------------------------
 
-def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None):
+def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None, lse=None):
     D = H * 64
     if o is None:
         o = torch.empty(B * N, D, dtype=qkv2d.dtype, device=qkv2d.device)
-    lse = torch.empty(B * H * N, dtype=torch.float32, device=qkv2d.device)
+    if lse is None:
+        lse = torch.empty(B * H * N, dtype=torch.float32, device=qkv2d.device)
     scale = 64 ** -0.5 if scale is None else scale
     call("vit_sdpa_fwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(lse),
          float(scale), _s(qkv2d))
     return o, lse
 
 
-def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None):
+def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None):
+    """dbias [3*H*64] (optional) receives the column sums of dqkv (the qkv bias gradient)."""
     if dqkv is None:
         dqkv = torch.empty_like(qkv2d)
     scale = 64 ** -0.5 if scale is None else scale
     delta = workspace("sdpa_delta", B * H * N * 4, qkv2d.device)
+    part, nfl = None, 0
+    if dbias is not None:
+        nfl = L.lib().vit_sdpa_bwd_partial_floats(B, N, H * 64)
+        part = workspace("sdpa_bias", nfl * 4, qkv2d.device)
     call("vit_sdpa_bwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(do),
-         do.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), ptr(delta), float(scale), _s(qkv2d))
+         do.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), ptr(delta), float(scale), ptr(dbias), ptr(part), nfl,
+         _s(qkv2d))
     return dqkv
 
 
