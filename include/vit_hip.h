@@ -98,16 +98,18 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
                        int64_t partial_floats, void* stream);
 int vit_layer_norm_bwd_partial_floats(int rows, int D);
 
-/* F.scaled_dot_product_attention(q,k,v) (timm Attention, no mask, head_dim 64,
- * N <= 288) reading q/k/v in place from the qkv GEMM output; lse [B*H*N] f32. */
+/* F.scaled_dot_product_attention(q,k,v) (timm Attention, head_dim 64, N <= 288) reading q/k/v in
+ * place from the qkv GEMM output; lse [B*H*N] f32.  causal = 1 masks key > query: the CLIP text
+ * tower's nn.MultiheadAttention attn_mask (NEWP:298 through the CLIP-HBA fork, external). */
 int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, void* o,
-                 int64_t ld_o, float* lse, float scale, void* stream);
+                 int64_t ld_o, float* lse, float scale, int causal, void* stream);
 /* SDPA backward into dqkv (qkv layout). delta_ws >= B*H*N floats.  dbias (optional, [3*H*64]) =
  * column sums of dqkv (the qkv Linear's bias gradient), fused into the kernels;
  * partial >= vit_sdpa_bwd_partial_floats(B, N, H*64). */
 int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, const void* o,
                  int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
-                 float* delta_ws, float scale, float* dbias, float* partial, int64_t partial_floats, void* stream);
+                 float* delta_ws, float scale, int causal, float* dbias, float* partial, int64_t partial_floats,
+                 void* stream);
 int vit_sdpa_bwd_partial_floats(int B, int N, int D);
 
 /* torch.nn.functional.cross_entropy(outputs, targets) mean (VIT:140) and its gradient. */
@@ -135,6 +137,25 @@ int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, 
 /* torch.optim.AdamW step (NEWP:1181): tensors {p, g, exp_avg, exp_avg_sq, n}[]. */
 int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, const float* lr, const float* step,
                    float beta1, float beta2, float eps, float weight_decay, void* stream);
+
+/* CLIP-HBA forward/loss around the towers (NEWP:287-304 -> clip_model(image, prompts, pos_embedding),
+ * the CLIP-HBA fork, external; OpenAI-CLIP semantics assumed):
+ *   token_embed   x[s*L+t] = table[tokens[s*L+t]] + pos[t]         (token_embedding + positional_embedding)
+ *   gather_rows   dst[i] = src[idx[i]]  (text EOT pooling x[arange, text.argmax(-1)], CLS rows)
+ *   scatter_rows  dst[idx[i]] = src[i]  (their backward; dst zeroed by the caller)
+ *   rownorm       y = exp(*log_scale) x / ||x|| (feature normalisation; log_scale null = 1), and backward
+ *   mse           nn.MSELoss() mean (NEWP:994, CBASE criterion) and its gradient (grad_loss null = 1) */
+int vit_token_embed(int rows, int L, int D, int vocab, const int64_t* tokens, const float* table, const float* pos,
+                    float* x, void* stream);
+int vit_gather_rows(int n, int D, const float* src, int64_t ld_src, const int64_t* idx, float* dst, int64_t ld_dst,
+                    void* stream);
+int vit_scatter_rows(int n, int D, const float* src, int64_t ld_src, const int64_t* idx, float* dst, int64_t ld_dst,
+                     void* stream);
+int vit_rownorm_fwd(int n, int D, const float* x, const float* log_scale, float* y, float* rnorm, void* stream);
+int vit_rownorm_bwd(int n, int D, const float* x, const float* dy, const float* rnorm, const float* log_scale,
+                    float* dx, void* stream);
+int vit_mse_fwd(int n, const float* pred, const float* target, float* loss, void* stream);
+int vit_mse_bwd(int n, const float* pred, const float* target, const float* grad_loss, float* dpred, void* stream);
 
 /* helpers */
 int vit_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);

@@ -15,6 +15,12 @@ What it pins:
        - DoRALayer.weight + autograd grads  (NEWP:407-463)    -> dora_golden.pt
        - behavioral_RSA                      (NEWP:605-654)    -> rsa_golden.npz
        - CosineAnnealingLRWithWarmup         (VIT:206-244)     -> lr_golden.json
+       - CLIPHBA.forward + DoRALayer + apply_dora_to_ViT + switch_dora_layers +
+         count_trainable_parameters (NEWP:268-304, 407-548) wrapped around a torch.nn
+         OpenAI-CLIP (nn.MultiheadAttention blocks) built from oracle/clip_ref.py's
+         parameters, one MSE + AdamW step                    -> clip_golden.pt
+       - shuffle_targets (NEWP:731-779) and the random-target / window rules of
+         train_model (NEWP:843-927), CPU generator          -> perturb_golden.pt
      The reference source itself is never copied; only input/output vectors are.
 """
 from __future__ import annotations
@@ -33,6 +39,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 from oracle import vit_ref as R  # noqa: E402
+from oracle import clip_ref as CR  # noqa: E402
 
 REF = "/root/reference"
 
@@ -217,8 +224,171 @@ def lr_fixture():
     return {"base_lr": 0.1, "warmup_epochs": 5, "max_epochs": 100, "lr_per_epoch": lrs}
 
 
+# ----------------------------------------------------------------------------
+# 3. CLIP-HBA: reference wrapper + DoRA functions around a torch.nn OpenAI-CLIP
+# ----------------------------------------------------------------------------
+
+class _TorchBlock(torch.nn.Module):
+    """OpenAI-CLIP ResidualAttentionBlock on torch.nn.MultiheadAttention (sequence-first)."""
+
+    def __init__(self, w, heads, mask):
+        super().__init__()
+        self.attn = torch.nn.MultiheadAttention(w, heads)
+        self.ln_1 = torch.nn.LayerNorm(w)
+        self.mlp = torch.nn.Sequential(OrderedDict([("c_fc", torch.nn.Linear(w, 4 * w)), ("gelu", _QuickGELU()),
+                                                    ("c_proj", torch.nn.Linear(4 * w, w))]))
+        self.ln_2 = torch.nn.LayerNorm(w)
+        self.attn_mask = mask
+
+    def forward(self, x):
+        m = None if self.attn_mask is None else self.attn_mask.to(x.dtype)
+        x = x + self.attn(self.ln_1(x), self.ln_1(x), self.ln_1(x), need_weights=False, attn_mask=m)[0]
+        return x + self.mlp(self.ln_2(x))
+
+
+class _QuickGELU(torch.nn.Module):
+    def forward(self, x):
+        return x * torch.sigmoid(1.702 * x)
+
+
+class _Seq(torch.nn.Module):
+    def __init__(self, w, layers, heads, mask):
+        super().__init__()
+        self.resblocks = torch.nn.Sequential(*[_TorchBlock(w, heads, mask) for _ in range(layers)])
+
+
+class _TorchCLIP(torch.nn.Module):
+    def __init__(self, cfg):
+        super().__init__()
+        vw, tw, L = cfg.vision_width, cfg.text_width, cfg.context_length
+        self.cfg = cfg
+        self.visual = torch.nn.Module()
+        self.visual.conv1 = torch.nn.Conv2d(3, vw, cfg.vision_patch, cfg.vision_patch, bias=False)
+        self.visual.class_embedding = torch.nn.Parameter(torch.empty(vw))
+        self.visual.positional_embedding = torch.nn.Parameter(torch.empty(cfg.vision_tokens, vw))
+        self.visual.ln_pre = torch.nn.LayerNorm(vw)
+        self.visual.transformer = _Seq(vw, cfg.vision_layers, cfg.vision_heads, None)
+        self.visual.ln_post = torch.nn.LayerNorm(vw)
+        self.visual.proj = torch.nn.Parameter(torch.empty(vw, cfg.embed_dim))
+        self.transformer = _Seq(tw, cfg.text_layers, cfg.text_heads, torch.empty(L, L).fill_(float("-inf")).triu_(1))
+        self.token_embedding = torch.nn.Embedding(cfg.vocab_size, tw)
+        self.positional_embedding = torch.nn.Parameter(torch.empty(L, tw))
+        self.ln_final = torch.nn.LayerNorm(tw)
+        self.text_projection = torch.nn.Parameter(torch.empty(tw, cfg.embed_dim))
+        self.logit_scale = torch.nn.Parameter(torch.ones([]))
+
+    def forward(self, image, text, pos_embedding):
+        v = self.visual
+        x = v.conv1(image).flatten(2).permute(0, 2, 1)
+        x = torch.cat([v.class_embedding + torch.zeros(x.shape[0], 1, x.shape[-1]), x], dim=1)
+        if pos_embedding:
+            x = x + v.positional_embedding
+        x = v.ln_pre(x).permute(1, 0, 2)
+        x = v.transformer.resblocks(x).permute(1, 0, 2)
+        img = v.ln_post(x[:, 0, :]) @ v.proj
+        text = text.reshape(-1, text.shape[-1])
+        t = (self.token_embedding(text) + self.positional_embedding).permute(1, 0, 2)
+        t = self.transformer.resblocks(t).permute(1, 0, 2)
+        t = self.ln_final(t)
+        txt = t[torch.arange(t.shape[0]), text.argmax(dim=-1)] @ self.text_projection
+        img = img / img.norm(dim=1, keepdim=True)
+        txt = txt / txt.norm(dim=1, keepdim=True)
+        return self.logit_scale.exp() * img @ txt.t()
+
+
+def _rel(a, b):
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-30))
+
+
+def clip_fixture():
+    _stub_reference_imports()
+    import functions.new_cvpr_train_behavior_things_pipeline as NEWP
+    cfg = CR.CLIP_TINY
+    seed, B, T, r = 21, 3, 5, 8
+    p = CR.init_params(cfg, seed=seed)
+    tclip = _TorchCLIP(cfg)
+    missing, unexpected = tclip.load_state_dict(p, strict=False)
+    assert not unexpected and not missing, (missing, unexpected)
+    g = torch.Generator().manual_seed(seed + 1)
+    image = torch.randn(B, 3, cfg.image_resolution, cfg.image_resolution, generator=g)
+    prompts = CR.synthetic_prompts(T, cfg, seed=seed + 2)
+    target = torch.randn(B, T, generator=g) * 3.0 + 1.0
+    # the reference wrapper, constructed without load_clip_to_cpu (network download)
+    m = NEWP.CLIPHBA.__new__(NEWP.CLIPHBA)
+    torch.nn.Module.__init__(m)
+    m.num_clip, m.clip_model, m.pos_embedding = T, tclip.float(), True
+    m.tokenized_prompts, m._cached_tokenized_prompts, m._cached_device = prompts, None, None
+    for q in m.clip_model.parameters():
+        q.requires_grad = False
+    torch.manual_seed(seed + 3)
+    NEWP.apply_dora_to_ViT(m, n_vision_layers=2, n_transformer_layers=1, r=r, dora_dropout=0.1)
+    NEWP.switch_dora_layers(m, freeze_all=True, dora_state=True)
+    count = NEWP.count_trainable_parameters(m)
+    names = sorted(n for n, q in m.named_parameters() if q.requires_grad)
+    # oracle DoRA init must agree with the reference's on m and D; A/B are copied over
+    dora = CR.init_dora(p, cfg, r=r, seed=seed + 4)
+    for n, mod in m.named_modules():
+        if isinstance(mod, NEWP.DoRALayer):
+            key = n
+            assert _rel(mod.m.detach(), dora[key + ".m"]) < 1e-6 and _rel(mod.D, dora[key + ".D"]) < 1e-6, key
+            with torch.no_grad():
+                mod.delta_D_A.copy_(dora[key + ".delta_D_A"])
+                mod.delta_D_B.copy_(dora[key + ".delta_D_B"])
+            assert mod.scaling == dora[key + ".scaling"]
+    opt = torch.optim.AdamW(m.parameters(), lr=3e-4)
+    opt.zero_grad()
+    pred = m(image)
+    loss = torch.nn.MSELoss()(pred, target)
+    loss.backward()
+    grads = {n: q.grad.detach().clone() for n, q in m.named_parameters() if q.requires_grad}
+    opt.step()
+    after = {n: q.detach().clone() for n, q in m.named_parameters() if q.requires_grad}
+    # oracle against the reference-wrapped torch.nn model
+    state = {}
+    d2 = OrderedDict((k, v.clone() if torch.is_tensor(v) else v) for k, v in dora.items())
+    oloss, opred, ograds = CR.train_step(p, d2, state, image, prompts, target, cfg, lr=3e-4)
+    print(f"  oracle vs reference CLIPHBA: pred rel {_rel(opred, pred.detach()):.3e}, "
+          f"loss {oloss:.6f} vs {float(loss):.6f}")
+    assert _rel(opred, pred.detach()) < 1e-5
+    for k in grads:
+        assert _rel(ograds[k], grads[k]) < 1e-4, (k, _rel(ograds[k], grads[k]))
+        assert _rel(d2[k], after[k]) < 1e-6, k
+    return {"seed": seed, "B": B, "T": T, "r": r, "cfg": cfg.__dict__,
+            "param_checksum": {k: float(v.double().sum()) for k, v in p.items()},
+            "image": image, "prompts": prompts, "target": target, "pred": pred.detach(), "loss": float(loss),
+            "grads": grads, "dora_after": after, "trainable_count": count, "trainable_names": names,
+            "dora_A_init": {k: dora[k] for k in dora if k.endswith(".delta_D_A")},
+            "dora_B_init": {k: dora[k] for k in dora if k.endswith(".delta_D_B")}}
+
+
+def perturb_fixture():
+    """shuffle_targets with a seeded CPU generator (NEWP:731-779, called at NEWP:959) and
+    the random_target draw (NEWP:919-927) on CPU generators; window rule NEWP:844-847."""
+    _stub_reference_imports()
+    import functions.new_cvpr_train_behavior_things_pipeline as NEWP
+    out = {"shuffle": [], "random_target": []}
+    targets = torch.randn(64, 66, generator=torch.Generator().manual_seed(5))
+    for (seed, run, batch) in [(0, 1, 0), (0, 37, 3), (1, 98, 22), (0, 136, 7)]:
+        s = seed + run * 1000 + batch
+        gen = torch.Generator()
+        gen.manual_seed(s)
+        out["shuffle"].append({"seed": s, "out": NEWP.shuffle_targets(targets, generator=gen)})
+        gen = torch.Generator()
+        gen.manual_seed(s)
+        out["random_target"].append({"seed": s, "normal": torch.randn(targets.shape, dtype=torch.float32,
+                                                                    generator=gen)})
+    out["targets"] = targets
+    return out
+
+
 def main():
     torch.set_num_threads(os.cpu_count() or 8)
+    only = sys.argv[1:]
+    if only:  # e.g. `make_golden.py clip perturb`: regenerate just those fixtures
+        for name in only:
+            fn = {"clip": (clip_fixture, "clip_golden.pt"), "perturb": (perturb_fixture, "perturb_golden.pt")}[name]
+            torch.save(fn[0](), os.path.join(HERE, fn[1]))
+        return
     print("ViT tiny fixture")
     torch.save(vit_fixture(R.VIT_TINY, B=3, seed=11, full_grads=True), os.path.join(HERE, "vit_tiny_golden.pt"))
     print("ViT-B/16 fixture (bs=2)")
@@ -230,6 +400,10 @@ def main():
     print("LR fixture (reference CosineAnnealingLRWithWarmup)")
     with open(os.path.join(HERE, "lr_golden.json"), "w") as f:
         json.dump(lr_fixture(), f, indent=1)
+    print("CLIP-HBA fixture (reference CLIPHBA/DoRA around torch.nn CLIP)")
+    torch.save(clip_fixture(), os.path.join(HERE, "clip_golden.pt"))
+    print("perturbation fixture (reference shuffle_targets)")
+    torch.save(perturb_fixture(), os.path.join(HERE, "perturb_golden.pt"))
     print("done")
 
 

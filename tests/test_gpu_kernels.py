@@ -289,6 +289,63 @@ def test_sdpa_fwd_bwd(N, dtype):
     _close(g[:, 2 * D:], dv, rel, "dv")
 
 
+@pytest.mark.parametrize("N", [77, 16, 197])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_sdpa_causal_fwd_bwd(N, dtype):
+    """Causal mask (CLIP text tower attn_mask: -inf above the diagonal) vs a torch fp32 reference."""
+    B, H = 3, 2
+    D = H * 64
+    qkv = _rnd(B * N, 3 * D, seed=44, scale=1.5).to(dtype)
+    do = _rnd(B * N, D, seed=45).to(dtype)
+    q, k, v = qkv.float().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    q, k, v = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    s = (q @ k.transpose(-2, -1)) * 0.125 + torch.full((N, N), float("-inf")).triu_(1)
+    lse_ref = torch.logsumexp(s, -1).reshape(-1)
+    o_ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * N, D)
+    o_ref.backward(do.float())
+    o, lse = ops.sdpa_fwd(qkv.to(DEV), B, H, N, causal=True)
+    _close(o, o_ref, 1e-5 if dtype == torch.float32 else 1.5e-2, "o")
+    _close(lse, lse_ref, 1e-5 if dtype == torch.float32 else 2e-3, "lse")
+    dqkv = ops.sdpa_bwd(qkv.to(DEV), o_ref.detach().to(dtype).to(DEV), do.to(DEV), lse_ref.detach().to(DEV), B, H, N,
+                        causal=True)
+    g = dqkv.float().cpu()
+    rel = 1e-4 if dtype == torch.float32 else 3e-2
+    for i, (name, ref) in enumerate((("dq", q.grad), ("dk", k.grad), ("dv", v.grad))):
+        _close(g[:, i * D:(i + 1) * D], ref.transpose(1, 2).reshape(B * N, D), rel, name)
+
+
+def test_clip_small_kernels():
+    """token embedding, row gather/scatter, feature rownorm fwd/bwd, MSE fwd/bwd vs torch fp32."""
+    g = torch.Generator().manual_seed(50)
+    S, Lq, D, V = 5, 16, 128, 64
+    tok = torch.randint(0, V, (S, Lq), generator=g)
+    table, pos = torch.randn(V, D, generator=g), torch.randn(Lq, D, generator=g)
+    x = ops.token_embed(tok.to(DEV), table.to(DEV), pos.to(DEV))
+    _close(x, (table[tok] + pos).reshape(S * Lq, D), 1e-6, "token_embed")
+    idx = torch.tensor([3, 17, 40, 79], dtype=torch.int64)
+    xg = ops.gather_rows(x, idx.to(DEV))
+    _close(xg, x.cpu()[idx], 0, "gather")
+    dst = ops.zero_(torch.empty(S * Lq, D, device=DEV))
+    ops.scatter_rows(xg, idx.to(DEV), dst)
+    ref = torch.zeros(S * Lq, D)
+    ref[idx] = x.cpu()[idx]
+    _close(dst, ref, 0, "scatter")
+    f = torch.randn(7, 96, generator=g).requires_grad_(True)
+    ls = torch.tensor([2.3])
+    y_ref = ls.exp() * f / f.norm(dim=1, keepdim=True)
+    dy = torch.randn(7, 96, generator=g)
+    y_ref.backward(dy)
+    y, rn = ops.rownorm_fwd(f.detach().to(DEV), ls.to(DEV))
+    _close(y, y_ref, 1e-5, "rownorm")
+    _close(ops.rownorm_bwd(f.detach().to(DEV), dy.to(DEV), rn, ls.to(DEV)), f.grad, 1e-5, "rownorm bwd")
+    p = torch.randn(64, 66, generator=g).requires_grad_(True)
+    t = torch.randn(64, 66, generator=g)
+    l_ref = torch.nn.functional.mse_loss(p, t)
+    l_ref.backward(torch.tensor(0.7))
+    _close(ops.mse_fwd(p.detach().to(DEV), t.to(DEV)).reshape(1), l_ref.detach().reshape(1), 1e-6, "mse")
+    _close(ops.mse_bwd(p.detach().to(DEV), t.to(DEV), torch.tensor(0.7, device=DEV)), p.grad, 1e-6, "mse bwd")
+
+
 # ---------------------------------------------------------------------------- CE / SGD / misc
 
 def test_cross_entropy():

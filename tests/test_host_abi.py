@@ -33,10 +33,14 @@ def test_library_exports_every_header_symbol():
     assert lib.vit_sgd_chunk_size() == 4096
 
 
-def test_library_is_gfx950_code_object():
+def test_library_is_gfx950_code_object(tmp_path):
+    import shutil
     import subprocess
     so = os.path.join(ROOT, "vit-project_amd", "vit_amd", "lib", "libvit_hip.so")
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", so], capture_output=True, text=True)
+    # --offloading extracts the device images next to its input: run it on a copy in tmp
+    cp = shutil.copy(so, tmp_path / "libvit_hip.so")
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(cp)], capture_output=True,
+                         text=True)
     assert "gfx950" in (out.stdout + out.stderr)
 
 

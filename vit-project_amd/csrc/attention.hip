@@ -1,6 +1,7 @@
 // Scaled-dot-product attention for timm Attention: per (batch, head)
-// softmax(q k^T * hd^-0.5) v with no mask, N <= 288 tokens (197 for ViT-B/16,
-// 257 for CLIP ViT-L/14), head_dim 64.
+// softmax(q k^T * hd^-0.5) v, N <= 288 tokens (197 for ViT-B/16, 257 for CLIP
+// ViT-L/14, 77 for the CLIP text tower), head_dim 64; unmasked or causal (the
+// text tower's build_attention_mask: key > query gets -inf).
 //
 // q/k/v are read in place from the fused qkv GEMM output [B*N, 3*D] (row stride
 // ld_qkv), the output o is written as [B*N, D] (the proj GEMM operand), and the
@@ -101,7 +102,7 @@ __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(
 template <int NT>  // key/query tiles of 16: NT = ceil(N/16)
 __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D,
                                                      int H, int N, float scale, bf16* __restrict__ o,
-                                                     int64_t ld_o, float* __restrict__ lse) {
+                                                     int64_t ld_o, float* __restrict__ lse, int causal) {
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128];
   char* Kimg = smem;
@@ -138,6 +139,13 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if ((NT - 1) * 16 + 4 * g + r >= N) s[NT - 1][r] = -INFINITY;
+    if (causal) {  // key > query masked (CLIP text tower attn_mask); key 0 always survives
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kt * 16 + 4 * g + r > q) s[kt][r] = -INFINITY;
+    }
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dq(const bf16* __restr
                                                             int64_t ld_o, const bf16* __restrict__ dout, int64_t ld_do,
                                                             const float* __restrict__ lse, float* __restrict__ delta_out,
                                                             bf16* __restrict__ dqkv, int64_t ld_dqkv,
-                                                            float* __restrict__ bias_part) {
+                                                            float* __restrict__ bias_part, int causal) {
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128];
   char* Kimg = smem;
@@ -284,6 +292,7 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dq(const bf16* __restr
         for (int r = 0; r < 4; ++r) {
           float pv = fexp2(fmaf(sacc[r], c2, -l2));
           if (edge && kt * 16 + 4 * g + r >= N) pv = 0.f;
+          if (causal && kt * 16 + 4 * g + r > q) pv = 0.f;
           ds[u][r] = pv * (dpacc[r] - dl);
         }
       }
@@ -310,7 +319,8 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
                                                              int N, float scale, const bf16* __restrict__ dout,
                                                              int64_t ld_do, const float* __restrict__ lse,
                                                              const float* __restrict__ delta_in, bf16* __restrict__ dqkv,
-                                                             int64_t ld_dqkv, float* __restrict__ bias_part) {
+                                                             int64_t ld_dqkv, float* __restrict__ bias_part,
+                                                             int causal) {
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128 + 2 * ROWS * 4];
   char* Qimg = smem;
@@ -366,7 +376,8 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
         const f32x4 dl = *reinterpret_cast<const f32x4*>(delta + qt * 16 + 4 * g);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float pv = kvalid ? fexp2(fmaf(sacc[r], c2, -l2[r])) : 0.f;
+          float pv = kvalid ? fexp2(fmaf(sacc[r], c2, -l2[r])) : 0.f;
+          if (causal && key > qt * 16 + 4 * g + r) pv = 0.f;
           p[u][r] = pv;
           ds[u][r] = pv * (dpacc[r] - dl[r]);
         }
@@ -404,7 +415,7 @@ constexpr int GCH = 64;  // rows per LDS chunk
 template <typename T>
 __global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ qkv, int64_t ld_qkv, int D, int H,
                                                         int N, float scale, T* __restrict__ o, int64_t ld_o,
-                                                        float* __restrict__ lse) {
+                                                        float* __restrict__ lse, int causal) {
   __shared__ float Ks[GCH][65], Vs[GCH][65];
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
   const int t = threadIdx.x, qi = blockIdx.x * 64 + (t >> 2), u = t & 3;
@@ -429,6 +440,7 @@ __global__ __launch_bounds__(256) void attn_fwd_generic(const T* __restrict__ qk
       for (int d = 0; d < 16; ++d) s = fmaf(qv[d], Ks[r][u * 16 + d], s);
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
+      if (causal && j0 + r > qi) s = -INFINITY;  // key 0 comes first, so m is finite from then on
       float mn = fmaxf(m, s);
       float corr = __expf(m - mn), p = __expf(s - mn);
       l = l * corr + p;
@@ -451,7 +463,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_generic(const T* __restrict__
                                                            int N, float scale, const T* __restrict__ o,
                                                            int64_t ld_o, const T* __restrict__ dout, int64_t ld_do,
                                                            const float* __restrict__ lse, float* __restrict__ delta_out,
-                                                           T* __restrict__ dqkv, int64_t ld_dqkv) {
+                                                           T* __restrict__ dqkv, int64_t ld_dqkv, int causal) {
   __shared__ float Ks[GCH][65], Vs[GCH][65];
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
   const int t = threadIdx.x, qi = blockIdx.x * 64 + (t >> 2), u = t & 3;
@@ -485,7 +497,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_generic(const T* __restrict__
       for (int d = 0; d < 16; ++d) { s = fmaf(qv[d], Ks[r][u * 16 + d], s); dp = fmaf(dov[d], Vs[r][u * 16 + d], dp); }
       s += __shfl_xor(s, 1, 64); s += __shfl_xor(s, 2, 64);
       dp += __shfl_xor(dp, 1, 64); dp += __shfl_xor(dp, 2, 64);
-      float ds = __expf(s - L) * (dp - dl);
+      float ds = (causal && j0 + r > qi) ? 0.f : __expf(s - L) * (dp - dl);
 #pragma unroll
       for (int d = 0; d < 16; ++d) acc[d] = fmaf(ds, Ks[r][u * 16 + d], acc[d]);
     }
@@ -503,7 +515,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_generic(const T* __restrict_
                                                             int N, float scale, const T* __restrict__ dout,
                                                             int64_t ld_do, const float* __restrict__ lse,
                                                             const float* __restrict__ delta, T* __restrict__ dqkv,
-                                                            int64_t ld_dqkv) {
+                                                            int64_t ld_dqkv, int causal) {
   __shared__ float Qs[GCH][65], Os[GCH][65];
   __shared__ float Ls[GCH], Dl[GCH];
   const int bh = blockIdx.y, b = bh / H, h = bh - b * H;
@@ -537,7 +549,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_generic(const T* __restrict_
       for (int d = 0; d < 16; ++d) { s = fmaf(Qs[r][u * 16 + d], kv[d], s); dp = fmaf(Os[r][u * 16 + d], vv[d], dp); }
       s += __shfl_xor(s, 1, 64); s += __shfl_xor(s, 2, 64);
       dp += __shfl_xor(dp, 1, 64); dp += __shfl_xor(dp, 2, 64);
-      float p = __expf(s * scale - Ls[r]);
+      float p = (causal && kj > i0 + r) ? 0.f : __expf(s * scale - Ls[r]);
       float ds = p * (dp - Dl[r]);
 #pragma unroll
       for (int d = 0; d < 16; ++d) { dv[d] = fmaf(p, Os[r][u * 16 + d], dv[d]); dk[d] = fmaf(ds, Qs[r][u * 16 + d], dk[d]); }
@@ -579,22 +591,22 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const T* __restrict__ o
 
 // ---------------------------------------------------------------------------
 template <int NT>
-static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, void* o,
+static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, int causal, void* o,
                     int64_t ld_o, float* lse, hipStream_t s) {
   hipLaunchKernelGGL((attn_fwd_mfma<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
-                     (bf16*)o, ld_o, lse);
+                     (bf16*)o, ld_o, lse, causal);
   VIT_CHECK_LAUNCH();
   return 0;
 }
 template <int NT>
-static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, const void* o,
+static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, int causal, const void* o,
                     int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, float* delta,
                     void* dqkv, int64_t ld_dqkv, float* bias_part, hipStream_t s) {
   hipLaunchKernelGGL((attn_bwd_dq<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
-                     (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, delta, (bf16*)dqkv, ld_dqkv, bias_part);
+                     (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, delta, (bf16*)dqkv, ld_dqkv, bias_part, causal);
   VIT_CHECK_LAUNCH();
   hipLaunchKernelGGL((attn_bwd_dkv<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
-                     (const bf16*)dout, ld_do, lse, (const float*)delta, (bf16*)dqkv, ld_dqkv, bias_part);
+                     (const bf16*)dout, ld_do, lse, (const float*)delta, (bf16*)dqkv, ld_dqkv, bias_part, causal);
   VIT_CHECK_LAUNCH();
   return 0;
 }
@@ -603,27 +615,28 @@ static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N,
 
 extern "C" {
 
-// F.scaled_dot_product_attention(q, k, v) (no mask, no dropout) for head_dim 64.
+// F.scaled_dot_product_attention(q, k, v) (no dropout) for head_dim 64; causal = 1
+// masks key > query (OpenAI CLIP text tower attn_mask, additive -inf above the diagonal).
 // qkv: [B*N, ld_qkv] with q at column h*64, k at D + h*64, v at 2D + h*64.
 // o: [B*N, ld_o] (column h*64); lse: [B*H*N] f32 (natural-log, scaled scores).
 int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, void* o,
-                 int64_t ld_o, float* lse, float scale, void* stream) {
+                 int64_t ld_o, float* lse, float scale, int causal, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (head_dim != 64 || N <= 0 || N > 288) return (int)hipErrorInvalidValue;
   const int D = H * 64;
   if (dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_o % 4 == 0)) {
     int nt = (N + 15) / 16;
     switch (nt) {
-#define CASE(n) case n: return fwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, lse, s);
+#define CASE(n) case n: return fwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, causal, o, ld_o, lse, s);
       NT_CASES(CASE)
 #undef CASE
     }
   }
   dim3 grid((N + 63) / 64, B * H);
   if (dtype == VIT_BF16)
-    hipLaunchKernelGGL(attn_fwd_generic<bf16>, grid, dim3(256), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale, (bf16*)o, ld_o, lse);
+    hipLaunchKernelGGL(attn_fwd_generic<bf16>, grid, dim3(256), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale, (bf16*)o, ld_o, lse, causal);
   else
-    hipLaunchKernelGGL(attn_fwd_generic<float>, grid, dim3(256), 0, s, (const float*)qkv, ld_qkv, D, H, N, scale, (float*)o, ld_o, lse);
+    hipLaunchKernelGGL(attn_fwd_generic<float>, grid, dim3(256), 0, s, (const float*)qkv, ld_qkv, D, H, N, scale, (float*)o, ld_o, lse, causal);
   VIT_CHECK_LAUNCH();
   return 0;
 }
@@ -641,7 +654,8 @@ int vit_sdpa_bwd_partial_floats(int B, int N, int D) {
 
 int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, const void* o,
                  int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
-                 float* delta_ws, float scale, float* dbias, float* partial, int64_t partial_floats, void* stream) {
+                 float* delta_ws, float scale, int causal, float* dbias, float* partial, int64_t partial_floats,
+                 void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (head_dim != 64 || N <= 0 || N > 288) return (int)hipErrorInvalidValue;
   const int D = H * 64;
@@ -651,7 +665,7 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
     int nt = (N + 15) / 16;
     int rc = (int)hipErrorInvalidValue;
     switch (nt) {
-#define CASE(n) case n: rc = bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, dbias ? partial : nullptr, s); break;
+#define CASE(n) case n: rc = bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, causal, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, dbias ? partial : nullptr, s); break;
       NT_CASES(CASE)
 #undef CASE
     }
@@ -663,10 +677,10 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
   dim3 grid((N + 63) / 64, B * H);
 #define GEN(T)                                                                                               \
   hipLaunchKernelGGL(attn_bwd_dq_generic<T>, grid, dim3(256), 0, s, (const T*)qkv, ld_qkv, D, H, N, scale,    \
-                     (const T*)o, ld_o, (const T*)dout, ld_do, lse, delta_ws, (T*)dqkv, ld_dqkv);            \
+                     (const T*)o, ld_o, (const T*)dout, ld_do, lse, delta_ws, (T*)dqkv, ld_dqkv, causal);    \
   VIT_CHECK_LAUNCH();                                                                                        \
   hipLaunchKernelGGL(attn_bwd_dkv_generic<T>, grid, dim3(256), 0, s, (const T*)qkv, ld_qkv, D, H, N, scale,   \
-                     (const T*)dout, ld_do, lse, delta_ws, (T*)dqkv, ld_dqkv);
+                     (const T*)dout, ld_do, lse, delta_ws, (T*)dqkv, ld_dqkv, causal);
   if (dtype == VIT_BF16) { GEN(bf16) } else { GEN(float) }
 #undef GEN
   VIT_CHECK_LAUNCH();

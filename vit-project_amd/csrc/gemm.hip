@@ -710,10 +710,15 @@ __global__ void colsum_partial_kernel(const T* __restrict__ X, int64_t ld, int M
 // host dispatch
 // ----------------------------------------------------------------------------
 // fast-path eligibility: bf16, 16-B aligned operands, 8-element row strides,
-// reduction length a multiple of BK (callers split off a ragged tail).
-static bool fast_ok(int dtype, int M, int N, int R, const void* P, const void* Q, int64_t ldp, int64_t ldq) {
+// reduction length a multiple of BK (callers split off a ragged tail).  An
+// r-contiguous (RC) operand's row count is free (staging clamps rows past the
+// edge, the epilogue guards i < M: e.g. the 66 x 77 = 5082 text-tower tokens);
+// an i/j-contiguous (CR) one loads 8-wide column chunks, so it needs a multiple
+// of 8; the 4-column epilogue stores need N % 4.
+static bool fast_ok(int dtype, int pl, int ql, int M, int N, int R, const void* P, const void* Q, int64_t ldp,
+                    int64_t ldq) {
   if (dtype != VIT_BF16) return false;
-  if (M % 8 || N % 8 || R % 32 || R <= 0) return false;
+  if ((pl == LAY_CR && M % 8) || (ql == LAY_CR && N % 8) || N % 4 || R % 32 || R <= 0) return false;
   if ((ldp % 8) || (ldq % 8)) return false;
   if (((uintptr_t)P & 15) || ((uintptr_t)Q & 15)) return false;
   return true;
@@ -813,7 +818,7 @@ static int gemm_dispatch(int dtype, int out_dtype, int pl, int ql, int M, int N,
                          const void* P, int64_t ldp, const void* Q, int64_t ldq, int split,
                          const Epi& e, hipStream_t s, bool allow_fast) {
   if (M <= 0 || N <= 0) return 0;
-  if (allow_fast && fast_ok(dtype, M, N, R, P, Q, ldp, ldq) && (e.ldc % 4 == 0)) {
+  if (allow_fast && fast_ok(dtype, pl, ql, M, N, R, P, Q, ldp, ldq) && (e.ldc % 4 == 0)) {
 #define FAST(PLx, QLx)                                                                                  \
     if (out_dtype == VIT_F32) return launch_fast<PLx, QLx, EPI, float, bf16>(P, ldp, Q, ldq, M, N, R, split, e, s); \
     else return launch_fast<PLx, QLx, EPI, bf16, bf16>(P, ldp, Q, ldq, M, N, R, split, e, s);
@@ -894,7 +899,7 @@ int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, con
   Epi e = make_epi();
   e.C = dX; e.ldc = lddx; e.aux = pre; e.ld_aux = lddx;
   const int rows = (M + 63) / 64;
-  const bool fast = fast_ok(dtype, M, K, N, dY, W, lddy, K) && (lddx % 4 == 0);
+  const bool fast = fast_ok(dtype, LAY_RC, LAY_CR, M, K, N, dY, W, lddy, K) && (lddx % 4 == 0);
   if (dbias) {
     if (partial == nullptr || partial_floats < vit_linear_dgrad_partial_floats(M, K)) return (int)hipErrorInvalidValue;
     if (fast) e.csum = partial;
@@ -933,7 +938,7 @@ int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t ldd
   if (M <= 0) return (int)hipMemsetAsync(dW, 0, (size_t)N * K * 4, s);
   // the MFMA kernel takes the BK-aligned rows; a ragged tail (M % 32) is added by the generic kernel
   const int tail = M % 32;
-  const bool fast = (M - tail) > 0 && fast_ok(dtype, N, K, M - tail, dY, X, lddy, ldx);
+  const bool fast = (M - tail) > 0 && fast_ok(dtype, LAY_CR, LAY_CR, N, K, M - tail, dY, X, lddy, ldx);
   const int R0 = fast ? M - tail : M;
   if (split > 1 && (workspace == nullptr || ws_bytes < (int64_t)split * N * K * 4)) return (int)hipErrorInvalidValue;
   Epi e = make_epi();

@@ -8,9 +8,12 @@ from .model import VisionTransformer, create_model, cross_entropy, set_wgrad_ove
 from .optim import FusedSGD, FusedAdamW, CosineAnnealingLRWithWarmup
 from .dora import DoRALayer, dora_weight
 from . import rsa
+from . import clip
+from .clip import CLIPHBA, MSELoss, mse_loss, apply_dora_to_ViT, switch_dora_layers, count_trainable_parameters
 
 __all__ = ["VisionTransformer", "create_model", "cross_entropy", "set_wgrad_overlap", "FusedSGD", "FusedAdamW",
-           "CosineAnnealingLRWithWarmup", "DoRALayer", "dora_weight", "rsa"]
+           "CosineAnnealingLRWithWarmup", "DoRALayer", "dora_weight", "rsa", "clip", "CLIPHBA", "MSELoss",
+           "mse_loss", "apply_dora_to_ViT", "switch_dora_layers", "count_trainable_parameters"]
 
 
 def load_library(path=None):

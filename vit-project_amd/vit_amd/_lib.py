@@ -38,8 +38,8 @@ SIGNATURES = {
     "vit_layer_norm_bwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, i32,
                            i32, vp, vp, vp, vp, i64, vp],
     "vit_layer_norm_bwd_partial_floats": [i32, i32],
-    "vit_sdpa_fwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, f32, vp],
-    "vit_sdpa_bwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, f32, vp, vp, i64, vp],
+    "vit_sdpa_fwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, f32, i32, vp],
+    "vit_sdpa_bwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, f32, i32, vp, vp, i64, vp],
     "vit_sdpa_bwd_partial_floats": [i32, i32, i32],
     "vit_patch_unfold": [i32, i32, i32, i32, i32, i32, vp, vp, vp],
     "vit_cls_pos_fill": [i32, i32, i32, vp, vp, vp, vp],
@@ -55,6 +55,13 @@ SIGNATURES = {
     "vit_dora_weight_fwd": [i32, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp],
     "vit_dora_weight_bwd": [i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp],
     "vit_adamw_step": [vp, vp, i32, vp, vp, f32, f32, f32, f32, vp],
+    "vit_token_embed": [i32, i32, i32, i32, vp, vp, vp, vp, vp],
+    "vit_gather_rows": [i32, i32, vp, i64, vp, vp, i64, vp],
+    "vit_scatter_rows": [i32, i32, vp, i64, vp, vp, i64, vp],
+    "vit_rownorm_fwd": [i32, i32, vp, vp, vp, vp, vp],
+    "vit_rownorm_bwd": [i32, i32, vp, vp, vp, vp, vp, vp],
+    "vit_mse_fwd": [i32, vp, vp, vp, vp],
+    "vit_mse_bwd": [i32, vp, vp, vp, vp, vp],
 }
 
 _lib = None

@@ -132,6 +132,20 @@ def _w(p: nn.Parameter):
     return p.detach() if sh is None else sh
 
 
+def _wt(p: torch.Tensor, dtype) -> torch.Tensor:
+    """The GEMM-dtype operand of a weight: its bf16 shadow if it has one (model parameters),
+    else a cast of the tensor itself (computed weights such as DoRALayer.weight)."""
+    sh = getattr(p, "_vit_shadow", None)
+    if sh is not None:
+        return sh
+    w = p.detach()
+    if w.dtype == dtype:
+        return w.contiguous()
+    out = torch.empty(w.shape, dtype=dtype, device=w.device)
+    ops.cast_bf16(w.contiguous(), out)
+    return out
+
+
 # ----------------------------------------------------------------------------
 # autograd nodes
 # ----------------------------------------------------------------------------
@@ -178,7 +192,13 @@ class _PatchEmbedFn(torch.autograd.Function):
 
 
 class _BlockFn(torch.autograd.Function):
-    """timm Block: x += proj(sdpa(qkv(norm1(x)))); x += fc2(gelu(fc1(norm2(x))))."""
+    """timm Block: x += proj(sdpa(qkv(norm1(x)))); x += fc2(gelu(fc1(norm2(x)))).
+
+    Also the OpenAI-CLIP ResidualAttentionBlock (same dataflow: nn.MultiheadAttention's
+    in_proj = qkv with the same [3, H, 64] row order, out_proj = proj, c_fc/c_proj = fc1/fc2,
+    QuickGELU, LN eps 1e-5, causal mask in the text tower).  The backward computes only what
+    ``ctx.needs_input_grad`` asks for: a frozen CLIP block whose only trainable input is a
+    DoRA ``out_proj.weight`` (NEWP:484-544) runs the MLP/LN2 backward and one wgrad."""
 
     @staticmethod
     def forward(ctx, x, n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b, cfg):
@@ -197,7 +217,8 @@ class _BlockFn(torch.autograd.Function):
         lse = torch.empty(B * H * N, dtype=f32, device=dev)
         xm, xo = torch.empty(M, D, dtype=f32, device=dev), torch.empty(M, D, dtype=f32, device=dev)
         pre, act = torch.empty(M, F, dtype=T, device=dev), torch.empty(M, F, dtype=T, device=dev)
-        Wqkv, Wproj, W1, W2 = _w(qkvw), _w(projw), _w(fc1w), _w(fc2w)
+        Wqkv, Wproj, W1, W2 = _wt(qkvw, T), _wt(projw, T), _wt(fc1w, T), _wt(fc2w, T)
+        causal = bool(cfg.get("causal", False))
 
         def chain(b0, b1):
             """The block over images [b0, b1): rows b0*N .. b1*N of every tensor."""
@@ -205,7 +226,7 @@ class _BlockFn(torch.autograd.Function):
             sl = slice(r0, r1_)
             ops.layer_norm_fwd(x2[sl], n1w.detach(), n1b.detach(), eps, T, out=h1[sl], mean=m1[sl], rstd=r1[sl])
             ops.linear_fwd(h1[sl], Wqkv, qkvb.detach(), out=qkv[sl])
-            ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N])
+            ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N], causal=causal)
             ops.linear_fwd(o[sl], Wproj, projb.detach(), epi=L.EPI_RESID, resid=x2[sl], out=xm[sl])
             ops.layer_norm_fwd(xm[sl], n2w.detach(), n2b.detach(), eps, T, out=h2[sl], mean=m2[sl], rstd=r2[sl])
             ops.linear_fwd(h2[sl], W1, fc1b.detach(), epi=act_epi, out=pre[sl], act_out=act[sl])
@@ -223,63 +244,77 @@ class _BlockFn(torch.autograd.Function):
             chain(0, B)
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, pre, act)
         ctx.params = (n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
-        ctx.meta = (B, N, D, H, T, cfg.get("compact_np", 0), cfg["quick_gelu"])
+        ctx.wops = (Wqkv, Wproj, W1, W2)
+        ctx.meta = (B, N, D, H, T, cfg.get("compact_np", 0), cfg["quick_gelu"], causal)
         return xo.reshape(B, N, D)
 
     @staticmethod
     def backward(ctx, dxo):
         x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, pre, act = ctx.saved_tensors
         n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b = ctx.params
-        B, N, D, H, T, compact_np, qg = ctx.meta
+        Wqkv, Wproj, W1, W2 = ctx.wops
+        B, N, D, H, T, compact_np, qg, causal = ctx.meta
+        ng = ctx.needs_input_grad
         M = B * N
+        dev = dxo.device
         dxo = dxo.contiguous().reshape(M, D)
         dxo_c, dxo_sum = _take_copy(dxo, T, want_dsum=True)
         gelu_bwd = L.EPI_QGELU_BWD if qg else L.EPI_GELU_BWD
-        side = _Side(dxo.device)
+        side = _Side(dev)
+        need_mlp_in = any(ng[0:11])     # anything upstream of fc2 (its input gradient path)
+        need_attn = any(ng[0:5])        # anything upstream of proj
+        need_h1 = any(ng[0:3])
         # gradient buffers are taken on the main stream (allocator ownership), filled on the side stream
-        g_fc2w, g_fc2b, g_fc1w, g_fc1b = _gout(fc2w), _gout(fc2b), _gout(fc1w), _gout(fc1b)
-        g_projw, g_projb, g_qkvw, g_qkvb = _gout(projw), _gout(projb), _gout(qkvw), _gout(qkvb)
+        g = [None] * 13
+        for i, p in ((1, n1w), (2, n1b), (3, qkvw), (4, qkvb), (5, projw), (6, projb), (7, n2w), (8, n2b),
+                     (9, fc1w), (10, fc1b), (11, fc2w), (12, fc2b)):
+            if ng[i]:
+                g[i] = _gout(p)
         # MLP.  Bias gradients are column sums fused into the kernels that produce each
         # gradient: fc2.bias from the upstream LayerNorm backward (side channel), fc1.bias
         # from the GELU' dgrad epilogue, proj.bias from LN2 backward, qkv.bias from SDPA backward.
-        if dxo_sum is not None:
-            d_fc2b = ops.colreduce(dxo_sum, 1, D, g_fc2b)
-        else:
-            d_fc2b = ops.colsum(dxo_c, out=g_fc2b)
-        d_fc2w = side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g_fc2w))
-        dpre = ops.linear_dgrad(dxo_c, _w(fc2w), out_dtype=T, epi=gelu_bwd, pre=pre, dbias=g_fc1b)
-        d_fc1b = g_fc1b
-        d_fc1w = side.run(lambda: ops.linear_wgrad(dpre, h2, out=g_fc1w))
-        dh2 = ops.linear_dgrad(dpre, _w(fc1w), out_dtype=T)
-        dxm = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
-        dxm_c = dxm if T == torch.float32 else torch.empty(M, D, dtype=T, device=dxo.device)
-        d_n2w, d_n2b = _gout(n2w), _gout(n2b)
-        ops.layer_norm_bwd(xm, D, dh2, n2w.detach(), m2, r2, dxm, D, M, dres=dxo, ldres=D,
-                           dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=d_n2w, dbeta=d_n2b,
-                           dsum=g_projb)
-        d_projb = g_projb
-        # attention
-        d_projw = side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g_projw))
-        do = ops.linear_dgrad(dxm_c, _w(projw), out_dtype=T)
-        dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g_qkvb)
-        d_qkvb = g_qkvb
-        d_qkvw = side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g_qkvw))
-        dh1 = ops.linear_dgrad(dqkv, _w(qkvw), out_dtype=T)
-        dx = torch.empty(M, D, dtype=torch.float32, device=dxo.device)
-        d_n1w, d_n1b = _gout(n1w), _gout(n1b)
-        if compact_np:
-            dx_c = torch.empty(B * compact_np, D, dtype=T, device=dxo.device)
-        else:
-            dx_c = None if T == torch.float32 else torch.empty(M, D, dtype=T, device=dxo.device)
-        # column sums of dx = the upstream block's fc2.bias gradient (not needed below the first block)
-        dsum = None if compact_np else torch.empty(D, dtype=torch.float32, device=dxo.device)
-        ops.layer_norm_bwd(x2, D, dh1, n1w.detach(), m1, r1, dx, D, M, dres=dxm, ldres=D, dx_copy=dx_c, ld_copy=D,
-                           compact_np=compact_np, dgamma=d_n1w, dbeta=d_n1b, dsum=dsum)
-        if dx_c is not None or dsum is not None:
-            _put_copy(dx, dx_c, dsum)
+        if ng[12]:
+            if dxo_sum is not None:
+                ops.colreduce(dxo_sum, 1, D, g[12])
+            else:
+                ops.colsum(dxo_c, out=g[12])
+        if ng[11]:
+            side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g[11]))
+        dx = None
+        if need_mlp_in:
+            dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=pre, dbias=g[10])
+            if ng[9]:
+                side.run(lambda: ops.linear_wgrad(dpre, h2, out=g[9]))
+        if any(ng[0:9]):
+            dh2 = ops.linear_dgrad(dpre, W1, out_dtype=T)
+            dxm = torch.empty(M, D, dtype=torch.float32, device=dev)
+            dxm_c = dxm if T == torch.float32 else torch.empty(M, D, dtype=T, device=dev)
+            ops.layer_norm_bwd(xm, D, dh2, n2w.detach(), m2, r2, dxm, D, M, dres=dxo, ldres=D,
+                               dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=g[7], dbeta=g[8],
+                               dsum=g[6])
+            # attention
+            if ng[5]:
+                side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5]))
+            if need_attn:
+                do = ops.linear_dgrad(dxm_c, Wproj, out_dtype=T)
+                dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g[4], causal=causal)
+                if ng[3]:
+                    side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g[3]))
+            if need_h1:
+                dh1 = ops.linear_dgrad(dqkv, Wqkv, out_dtype=T)
+                dx = torch.empty(M, D, dtype=torch.float32, device=dev)
+                if compact_np:
+                    dx_c = torch.empty(B * compact_np, D, dtype=T, device=dev)
+                else:
+                    dx_c = None if T == torch.float32 or not ng[0] else torch.empty(M, D, dtype=T, device=dev)
+                # column sums of dx = the upstream block's fc2.bias gradient (not needed below the first block)
+                dsum = None if (compact_np or not ng[0]) else torch.empty(D, dtype=torch.float32, device=dev)
+                ops.layer_norm_bwd(x2, D, dh1, n1w.detach(), m1, r1, dx, D, M, dres=dxm, ldres=D, dx_copy=dx_c,
+                                   ld_copy=D, compact_np=compact_np, dgamma=g[1], dbeta=g[2], dsum=dsum)
+                if ng[0] and (dx_c is not None or dsum is not None):
+                    _put_copy(dx, dx_c, dsum)
         side.join()
-        return (dx.reshape(B, N, D), d_n1w, d_n1b, d_qkvw, d_qkvb, d_projw, d_projb, d_n2w, d_n2b, d_fc1w,
-                d_fc1b, d_fc2w, d_fc2b, None)
+        return (dx.reshape(B, N, D) if (ng[0] and dx is not None) else None, *g[1:], None)
 
 
 class _HeadFn(torch.autograd.Function):

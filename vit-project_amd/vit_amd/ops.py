@@ -162,7 +162,7 @@ def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0
 # attention
 # ----------------------------------------------------------------------------
 
-def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None, lse=None):
+def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None, lse=None, causal=False):
     D = H * 64
     if o is None:
         o = torch.empty(B * N, D, dtype=qkv2d.dtype, device=qkv2d.device)
@@ -170,11 +170,11 @@ def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None, lse=None):
         lse = torch.empty(B * H * N, dtype=torch.float32, device=qkv2d.device)
     scale = 64 ** -0.5 if scale is None else scale
     call("vit_sdpa_fwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(lse),
-         float(scale), _s(qkv2d))
+         float(scale), int(causal), _s(qkv2d))
     return o, lse
 
 
-def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None):
+def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None, causal=False):
     """dbias [3*H*64] (optional) receives the column sums of dqkv (the qkv bias gradient)."""
     if dqkv is None:
         dqkv = torch.empty_like(qkv2d)
@@ -185,8 +185,8 @@ def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None):
         nfl = L.lib().vit_sdpa_bwd_partial_floats(B, N, H * 64)
         part = workspace("sdpa_bias", nfl * 4, qkv2d.device)
     call("vit_sdpa_bwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(do),
-         do.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), ptr(delta), float(scale), ptr(dbias), ptr(part), nfl,
-         _s(qkv2d))
+         do.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), ptr(delta), float(scale), int(causal), ptr(dbias),
+         ptr(part), nfl, _s(qkv2d))
     return dqkv
 
 
@@ -243,3 +243,71 @@ def cast_bf16(src: torch.Tensor, dst: torch.Tensor):
 def zero_(t: torch.Tensor):
     call("vit_zero", ptr(t), t.numel() * t.element_size(), _s(t))
     return t
+
+
+# ----------------------------------------------------------------------------
+# CLIP-HBA pieces (csrc/clip.hip)
+# ----------------------------------------------------------------------------
+
+def token_embed(tokens, table, pos):
+    """x [S*L, D] f32 = table[tokens] + pos[t]  (tokens int64 [S, L])."""
+    S, Lq = tokens.shape
+    D = table.shape[1]
+    x = torch.empty(S * Lq, D, dtype=torch.float32, device=table.device)
+    call("vit_token_embed", S * Lq, Lq, D, table.shape[0], ptr(tokens.contiguous()), ptr(table), ptr(pos), ptr(x),
+         _s(table))
+    return x
+
+
+def gather_rows(src2d, idx, out=None):
+    n = idx.numel()
+    D = src2d.shape[1]
+    if out is None:
+        out = torch.empty(n, D, dtype=torch.float32, device=src2d.device)
+    call("vit_gather_rows", n, D, ptr(src2d), src2d.stride(0), ptr(idx), ptr(out), out.stride(0), _s(src2d))
+    return out
+
+
+def scatter_rows(src2d, idx, dst2d):
+    n = idx.numel()
+    call("vit_scatter_rows", n, src2d.shape[1], ptr(src2d), src2d.stride(0), ptr(idx), ptr(dst2d), dst2d.stride(0),
+         _s(src2d))
+    return dst2d
+
+
+def rownorm_fwd(x2d, log_scale=None):
+    n, D = x2d.shape
+    y = torch.empty_like(x2d)
+    rn = torch.empty(n, dtype=torch.float32, device=x2d.device)
+    call("vit_rownorm_fwd", n, D, ptr(x2d), ptr(log_scale), ptr(y), ptr(rn), _s(x2d))
+    return y, rn
+
+
+def rownorm_bwd(x2d, dy, rn, log_scale=None):
+    n, D = x2d.shape
+    dx = torch.empty_like(x2d)
+    call("vit_rownorm_bwd", n, D, ptr(x2d), ptr(dy.contiguous()), ptr(rn), ptr(log_scale), ptr(dx), _s(x2d))
+    return dx
+
+
+def mse_fwd(pred, target):
+    loss = torch.empty((), dtype=torch.float32, device=pred.device)
+    call("vit_mse_fwd", pred.numel(), ptr(pred), ptr(target), ptr(loss), _s(pred))
+    return loss
+
+
+def mse_bwd(pred, target, grad_loss=None):
+    d = torch.empty_like(pred)
+    g = grad_loss.to(torch.float32).contiguous() if grad_loss is not None else None
+    call("vit_mse_bwd", pred.numel(), ptr(pred), ptr(target), ptr(g), ptr(d), _s(pred))
+    return d
+
+
+def gemm(P, p_layout, Q, q_layout, M, N, R, out=None, out_dtype=torch.float32, bias=None):
+    """Raw C[i][j] = sum_r P(i,r) Q(j,r) (+bias[j]); layouts L.LAY_RC (r contiguous) / L.LAY_CR."""
+    assert P.dtype == Q.dtype and P.stride(-1) == 1 and Q.stride(-1) == 1
+    if out is None:
+        out = torch.empty(M, N, dtype=out_dtype, device=P.device)
+    call("vit_gemm", L.dt(P), L.dt(out), p_layout, q_layout, L.EPI_STORE, M, N, R, ptr(P), P.stride(0), ptr(Q),
+         Q.stride(0), ptr(out), out.stride(0), ptr(bias), None, 0, None, 1, _s(P))
+    return out
