@@ -27,11 +27,11 @@ enum { VIT_DTYPE_F32 = 0, VIT_DTYPE_BF16 = 1 };
 enum { VIT_LAYOUT_RC = 0, VIT_LAYOUT_CR = 1 };
 enum {
   VIT_EPI_STORE = 0,      /* C = acc (+bias)                                   */
-  VIT_EPI_BIAS_GELU = 1,  /* C = pre = acc+bias, aux_out = gelu_erf(pre)       */
+  VIT_EPI_BIAS_GELU = 1,  /* pre = acc+bias: C = gelu_erf'(pre), aux_out = gelu_erf(pre) */
   VIT_EPI_RESID = 2,      /* C (f32) = resid + acc + bias                      */
-  VIT_EPI_GELU_BWD = 3,   /* C = acc * gelu_erf'(pre)                          */
+  VIT_EPI_GELU_BWD = 3,   /* C = acc * aux (aux = the gelu'(pre) BIAS_GELU saved) */
   VIT_EPI_PATCH = 4,      /* patch-embed row remap + pos_embed                 */
-  VIT_EPI_BIAS_QGELU = 5, /* QuickGELU variant (OpenAI CLIP towers)            */
+  VIT_EPI_BIAS_QGELU = 5, /* QuickGELU variant (OpenAI CLIP towers): C = qgelu'(pre) */
   VIT_EPI_QGELU_BWD = 6
 };
 

@@ -26,6 +26,11 @@ def _close(got, ref, rel, what=""):
     assert err <= rel * scale, f"{what}: max err {err:.3e} > {rel:.1e} * scale {scale:.3e}"
 
 
+def _gelu_grad(x):
+    """d/dx of exact-erf GELU."""
+    return 0.5 * (1 + torch.erf(x / 2 ** 0.5)) + x * torch.exp(-0.5 * x * x) / (2 * torch.pi) ** 0.5
+
+
 def _rnd(*shape, dtype=torch.float32, seed=0, scale=1.0):
     g = torch.Generator().manual_seed(seed)
     return (torch.randn(*shape, generator=g) * scale).to(dtype)
@@ -66,9 +71,9 @@ def test_linear_epilogues_bf16():
     w = _rnd(N, K, seed=5, scale=0.06, dtype=torch.bfloat16)
     b = _rnd(N, seed=6, scale=0.1)
     acc = x.float() @ w.float().T + b
-    pre, act = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_BIAS_GELU)
-    _close(pre, acc, 8e-3, "pre")
-    _close(act, torch.nn.functional.gelu(pre.float().cpu()), 8e-3, "gelu")
+    dact, act = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_BIAS_GELU)
+    _close(act, torch.nn.functional.gelu(acc), 8e-3, "gelu")
+    _close(dact, _gelu_grad(acc), 8e-3, "gelu'")
     resid = _rnd(M, N, seed=7)
     out = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_RESID, resid=resid.to(DEV))
     _close(out, resid + acc, 1e-5, "resid")
@@ -77,9 +82,10 @@ def test_linear_epilogues_bf16():
     ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_RESID, resid=r2, out=r2)
     _close(r2, resid + acc, 1e-5, "resid inplace")
     # quick gelu
-    pre_q, act_q = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_BIAS_QGELU)
-    p = pre_q.float().cpu()
-    _close(act_q, p * torch.sigmoid(1.702 * p), 8e-3, "qgelu")
+    dq, act_q = ops.linear_fwd(x.to(DEV), w.to(DEV), b.to(DEV), epi=L.EPI_BIAS_QGELU)
+    s = torch.sigmoid(1.702 * acc)
+    _close(act_q, acc * s, 8e-3, "qgelu")
+    _close(dq, s + 1.702 * acc * s * (1 - s), 8e-3, "qgelu'")
 
 
 def test_linear_dgrad_and_gelu_bwd():
@@ -93,7 +99,9 @@ def test_linear_dgrad_and_gelu_bwd():
     pf = pre.float().requires_grad_(True)
     torch.nn.functional.gelu(pf).backward(ref)
     db = torch.empty(K, device=DEV)
-    d = ops.linear_dgrad(dy.to(DEV), w.to(DEV), out_dtype=torch.bfloat16, epi=L.EPI_GELU_BWD, pre=pre.to(DEV),
+    # the forward epilogue saves gelu'(pre); the dgrad epilogue multiplies by it
+    dact = _gelu_grad(pre.float()).to(torch.bfloat16)
+    d = ops.linear_dgrad(dy.to(DEV), w.to(DEV), out_dtype=torch.bfloat16, epi=L.EPI_GELU_BWD, pre=dact.to(DEV),
                          dbias=db)
     _close(d, pf.grad, 8e-3, "gelu bwd")
     _close(db, pf.grad.sum(0), 1e-3, "fused bias grad (MFMA epilogue)")
@@ -136,9 +144,9 @@ def test_gemm_every_tile_config(variant):
     lib.vit_gemm_variant(variant)
     try:
         ref = x.float() @ w.float().T + b
-        pre, act = ops.linear_fwd(xd, wd, bd, epi=L.EPI_BIAS_GELU)
-        _close(pre, ref, 1e-2, "pre")
-        _close(act, torch.nn.functional.gelu(pre.float().cpu()), 1e-2, "gelu")
+        dact, act = ops.linear_fwd(xd, wd, bd, epi=L.EPI_BIAS_GELU)
+        _close(act, torch.nn.functional.gelu(ref), 1e-2, "gelu")
+        _close(dact, _gelu_grad(ref), 1e-2, "gelu'")
         out = res.to(DEV).clone()
         ops.linear_fwd(xd, wd, bd, epi=L.EPI_RESID, resid=out, out=out)
         _close(out, ref + res, 1e-5, "resid")

@@ -73,7 +73,32 @@ __device__ __forceinline__ float gelu_fast(float x) { return 0.5f * x * (1.0f + 
 __device__ __forceinline__ float gelu_fast_grad(float x) {
   return 0.5f * (1.0f + erf_fast(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
 }
+// GELU and its derivative from one erf evaluation (the forward epilogue stores both:
+// the activation for fc2 and GELU'(pre) for the backward's dgrad epilogue).
+__device__ __forceinline__ void gelu_fast_both(float x, float& g, float& gp) {
+  const float z = x * 0.70710678118654752f;
+  const float az = fabsf(z);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, az, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  const float e = __expf(-az * az);  // exp(-x^2 / 2)
+  const float cdf = 0.5f + 0.5f * copysignf(1.0f - p * t * e, z);
+  g = x * cdf;
+  gp = fmaf(x * 0.39894228040143268f, e, cdf);
+}
+__device__ __forceinline__ void gelu_erf_both(float x, float& g, float& gp) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
+  g = x * cdf;
+  gp = cdf + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+}
 __device__ __forceinline__ float quick_gelu(float x) { return x / (1.0f + __expf(-1.702f * x)); }
+__device__ __forceinline__ void quick_gelu_both(float x, float& g, float& gp) {
+  const float s = 1.0f / (1.0f + __expf(-1.702f * x));
+  g = x * s;
+  gp = s + 1.702f * x * s * (1.0f - s);
+}
 __device__ __forceinline__ float quick_gelu_grad(float x) {
   float s = 1.0f / (1.0f + __expf(-1.702f * x));
   return s + 1.702f * x * s * (1.0f - s);

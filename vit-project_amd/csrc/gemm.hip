@@ -23,6 +23,8 @@
 #include <type_traits>
 
 enum { LAY_RC = 0, LAY_CR = 1 };
+// BIAS_GELU / BIAS_QGELU: C = act'(pre) (what the backward needs), aux_out = act(pre);
+// GELU_BWD / QGELU_BWD: C = acc * aux, aux = that saved act'(pre)  (same for both).
 enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_PATCH = 4,
        EPI_BIAS_QGELU = 5, EPI_QGELU_BWD = 6, EPI_ACC = 7 };
 
@@ -70,14 +72,19 @@ __device__ __forceinline__ f32x4 epi4(const Epi& e, int i, int j, f32x4 v, int z
     store4<TO>(c, v + load4<TO>(c));
     return v;
   } else if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) {
-    // the activation is computed from the rounded pre-activation that backward sees
-    store4<TO>((TO*)e.C + (int64_t)i * e.ldc + j, v);
-    f32x4 pre_r;
+    // act and act' of the pre-activation rounded to the storage type (the value a
+    // stored-pre design would have differentiated)
+    f32x4 a, d;
 #pragma unroll
-    for (int t = 0; t < 4; ++t) pre_r[t] = (float)(TO)v[t];
-    f32x4 a;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) a[t] = (EPI == EPI_BIAS_GELU) ? gelu_fast(pre_r[t]) : quick_gelu(pre_r[t]);
+    for (int t = 0; t < 4; ++t) {
+      const float pr = (float)(TO)v[t];
+      float ga, gd;
+      if constexpr (EPI == EPI_BIAS_GELU) gelu_fast_both(pr, ga, gd);
+      else quick_gelu_both(pr, ga, gd);
+      a[t] = ga;
+      d[t] = gd;
+    }
+    store4<TO>((TO*)e.C + (int64_t)i * e.ldc + j, d);
     store4<TO>((TO*)e.aux_out + (int64_t)i * e.ldc + j, a);
     return v;
   } else if constexpr (EPI == EPI_RESID) {
@@ -85,9 +92,7 @@ __device__ __forceinline__ f32x4 epi4(const Epi& e, int i, int j, f32x4 v, int z
     store4<TO>((TO*)e.C + (int64_t)i * e.ldc + j, v + r);
     return v;
   } else if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
-    f32x4 pre = load4<TA>((const TA*)e.aux + (int64_t)i * e.ld_aux + j);
-#pragma unroll
-    for (int t = 0; t < 4; ++t) v[t] *= (EPI == EPI_GELU_BWD) ? gelu_fast_grad(pre[t]) : quick_gelu_grad(pre[t]);
+    v *= load4<TA>((const TA*)e.aux + (int64_t)i * e.ld_aux + j);
     store4<TO>((TO*)e.C + (int64_t)i * e.ldc + j, v);
   } else if constexpr (EPI == EPI_PATCH) {
     int b = i / e.n_patch, p = i - b * e.n_patch;
@@ -123,6 +128,175 @@ __device__ __forceinline__ void csum_flush(const Epi& e, f32x4 (&cs)[AJ], int ro
   }
 }
 
+// ---------------------------------------------------------------------------
+// Row-contiguous epilogue (the bf16 fast kernels): V = 16 / sizeof(TO) consecutive
+// columns j..j+V-1 of row i per thread, so every global load and store is 16 B and
+// a wave's instruction covers whole 512-B row segments (the MFMA fragment layout
+// gives 8-B pieces of 16 different rows per instruction: store-issue-bound).
+// ---------------------------------------------------------------------------
+template <int V> struct VecF { f32x4 q[V / 4]; };
+
+template <typename T, int V> __device__ __forceinline__ void vload(const T* p, VecF<V>& v);
+template <> __device__ __forceinline__ void vload<float, 4>(const float* p, VecF<4>& v) {
+  v.q[0] = *reinterpret_cast<const f32x4*>(p);
+}
+template <> __device__ __forceinline__ void vload<float, 8>(const float* p, VecF<8>& v) {
+  v.q[0] = *reinterpret_cast<const f32x4*>(p);
+  v.q[1] = *reinterpret_cast<const f32x4*>(p + 4);
+}
+template <> __device__ __forceinline__ void vload<bf16, 8>(const bf16* p, VecF<8>& v) {
+  const bf16x8 x = *reinterpret_cast<const bf16x8*>(p);
+  v.q[0] = f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+  v.q[1] = f32x4{(float)x[4], (float)x[5], (float)x[6], (float)x[7]};
+}
+template <> __device__ __forceinline__ void vload<bf16, 4>(const bf16* p, VecF<4>& v) {
+  const bf16x4 x = *reinterpret_cast<const bf16x4*>(p);
+  v.q[0] = f32x4{(float)x[0], (float)x[1], (float)x[2], (float)x[3]};
+}
+template <typename T, int V> __device__ __forceinline__ void vstore(T* p, const VecF<V>& v);
+template <> __device__ __forceinline__ void vstore<float, 4>(float* p, const VecF<4>& v) {
+  *reinterpret_cast<f32x4*>(p) = v.q[0];
+}
+template <> __device__ __forceinline__ void vstore<bf16, 8>(bf16* p, const VecF<8>& v) {
+  const bf16x8 o = {(bf16)v.q[0][0], (bf16)v.q[0][1], (bf16)v.q[0][2], (bf16)v.q[0][3],
+                    (bf16)v.q[1][0], (bf16)v.q[1][1], (bf16)v.q[1][2], (bf16)v.q[1][3]};
+  *reinterpret_cast<bf16x8*>(p) = o;
+}
+
+// Epilogue math on V columns; returns (in v) the value whose column sum a fused
+// bias gradient wants (what was stored as C, before a GELU activation).
+template <int EPI, typename TO, typename TA, int V>
+__device__ __forceinline__ void epi_vec(const Epi& e, int i, int j, VecF<V>& v, int z) {
+  if (e.bias) {
+    VecF<V> b;
+    vload<float, V>(e.bias + j, b);
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q) v.q[q] += b.q[q];
+  }
+  if constexpr (EPI == EPI_STORE) {
+    vstore<TO, V>((TO*)e.C + e.slab * z + (int64_t)i * e.ldc + j, v);
+  } else if constexpr (EPI == EPI_ACC) {
+    TO* c = (TO*)e.C + (int64_t)i * e.ldc + j;
+    VecF<V> o;
+    vload<TO, V>(c, o);
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q) o.q[q] += v.q[q];
+    vstore<TO, V>(c, o);
+  } else if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) {
+    VecF<V> a, d;
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float pr = (float)(TO)v.q[q][t];  // pre-activation rounded to the storage type
+        float ga, gd;
+        if constexpr (EPI == EPI_BIAS_GELU) gelu_fast_both(pr, ga, gd);
+        else quick_gelu_both(pr, ga, gd);
+        a.q[q][t] = ga;
+        d.q[q][t] = gd;
+      }
+    vstore<TO, V>((TO*)e.C + (int64_t)i * e.ldc + j, d);
+    vstore<TO, V>((TO*)e.aux_out + (int64_t)i * e.ldc + j, a);
+  } else if constexpr (EPI == EPI_RESID) {
+    VecF<V> r;
+    vload<float, V>((const float*)e.aux + (int64_t)i * e.ld_aux + j, r);
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q) r.q[q] += v.q[q];
+    vstore<TO, V>((TO*)e.C + (int64_t)i * e.ldc + j, r);
+  } else if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+    VecF<V> dact;
+    vload<TA, V>((const TA*)e.aux + (int64_t)i * e.ld_aux + j, dact);
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q) v.q[q] *= dact.q[q];
+    vstore<TO, V>((TO*)e.C + (int64_t)i * e.ldc + j, v);
+  } else if constexpr (EPI == EPI_PATCH) {
+    const int b = i / e.n_patch, p = i - b * e.n_patch;
+    const int64_t row = (int64_t)b * (e.n_patch + 1) + 1 + p;
+    VecF<V> ps;
+    vload<float, V>(e.pos + (int64_t)(1 + p) * e.ldc + j, ps);
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q) ps.q[q] += v.q[q];
+    vstore<TO, V>((TO*)e.C + row * e.ldc + j, ps);
+  }
+}
+
+// LDS bytes the staged epilogue of a BM x BN tile needs: one WM-row band of f32
+// accumulators (rows padded by 16 B) + the column-sum reduction rows.
+template <class C, typename TO> struct EpiLds {
+  static constexpr int V = 16 / (int)sizeof(TO);
+  static constexpr int ROWB = C::BN * 4 + 16;
+  static constexpr int CPR = C::BN / V;           // V-column chunks per row
+  static constexpr int RL = C::THREADS / CPR;     // rows in flight per sweep
+  static constexpr int STAGE = C::WM * ROWB;
+  static constexpr int BYTES = STAGE + RL * C::BN * 4;
+  static_assert(C::THREADS % CPR == 0 && C::WM % RL == 0 && 64 % RL == 0, "epilogue sweep shape");
+};
+
+// Staged epilogue: for each band of WM rows (the waves of one wi), those waves
+// write their f32 accumulators to LDS, then the whole workgroup sweeps the band
+// row-contiguously through epi_vec.  Column sums (fused bias gradients) are
+// reduced over each 64-row group through LDS and written as one partial row.
+template <class C, int EPI, typename TO, typename TA>
+__device__ __forceinline__ void epilogue_staged(const Epi& e, const f32x4 (&acc)[C::AI][C::AJ], char* smem, int i0,
+                                                int j0, int wi, int wj, int lane, int M, int N, int z) {
+  using EL = EpiLds<C, TO>;
+  constexpr int V = EL::V;
+  const int tid = threadIdx.x;
+  const int c = tid % EL::CPR, r0 = tid / EL::CPR;
+  float* red = reinterpret_cast<float*>(smem + EL::STAGE);
+  const int j = j0 + c * V;
+#pragma unroll 1
+  for (int p = 0; p < C::WI; ++p) {
+    __syncthreads();  // main-loop fragment reads / the previous band's sweep are done
+    if (wi == p) {
+#pragma unroll
+      for (int a = 0; a < C::AI; ++a)
+#pragma unroll
+        for (int b = 0; b < C::AJ; ++b) {
+          const int row = a * 16 + (lane & 15), col = wj * C::WN + b * 16 + 4 * (lane >> 4);
+          *reinterpret_cast<f32x4*>(smem + row * EL::ROWB + col * 4) = acc[a][b];
+        }
+    }
+    __syncthreads();
+    const int ib = i0 + p * C::WM;
+    VecF<V> cs;
+#pragma unroll
+    for (int q = 0; q < V / 4; ++q) cs.q[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int r = r0; r < C::WM; r += EL::RL) {
+      VecF<V> v;
+      const float* src = reinterpret_cast<const float*>(smem + r * EL::ROWB) + c * V;
+#pragma unroll
+      for (int q = 0; q < V / 4; ++q) v.q[q] = *reinterpret_cast<const f32x4*>(src + 4 * q);
+      const int i = ib + r;
+      if (i < M && j < N) {
+        epi_vec<EPI, TO, TA, V>(e, i, j, v, z);
+        if (e.csum) {
+#pragma unroll
+          for (int q = 0; q < V / 4; ++q) cs.q[q] += v.q[q];
+        }
+      }
+      if (e.csum && ((r + EL::RL) & 63) < EL::RL) {  // last row of this thread in a 64-row group
+        float* rr = red + r0 * C::BN + c * V;
+#pragma unroll
+        for (int q = 0; q < V / 4; ++q) {
+          *reinterpret_cast<f32x4*>(rr + 4 * q) = cs.q[q];
+          cs.q[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        __syncthreads();
+        const int g0 = ib + (r & ~63);
+        for (int col = tid; col < C::BN; col += C::THREADS) {
+          float sum = 0.f;
+#pragma unroll
+          for (int k = 0; k < EL::RL; ++k) sum += red[k * C::BN + col];
+          if (g0 < M && j0 + col < N) e.csum[(int64_t)(g0 >> 6) * N + j0 + col] = sum;
+        }
+        __syncthreads();
+      }
+    }
+  }
+}
+
 // Scalar form for the generic kernel (ragged edges).
 template <int EPI, typename TO, typename TA>
 __device__ __forceinline__ void epi1(const Epi& e, int i, int j, float v) {
@@ -133,15 +307,16 @@ __device__ __forceinline__ void epi1(const Epi& e, int i, int j, float v) {
     TO* c = (TO*)e.C + (int64_t)i * e.ldc + j;
     *c = (TO)((float)*c + v);
   } else if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) {
-    TO pr = (TO)v;
-    ((TO*)e.C)[(int64_t)i * e.ldc + j] = pr;
-    float pf = (float)pr;
-    ((TO*)e.aux_out)[(int64_t)i * e.ldc + j] = (TO)((EPI == EPI_BIAS_GELU) ? gelu_erf(pf) : quick_gelu(pf));
+    const float pf = (float)(TO)v;
+    float a, d;
+    if constexpr (EPI == EPI_BIAS_GELU) gelu_erf_both(pf, a, d);
+    else quick_gelu_both(pf, a, d);
+    ((TO*)e.C)[(int64_t)i * e.ldc + j] = (TO)d;
+    ((TO*)e.aux_out)[(int64_t)i * e.ldc + j] = (TO)a;
   } else if constexpr (EPI == EPI_RESID) {
     ((TO*)e.C)[(int64_t)i * e.ldc + j] = (TO)(v + ((const float*)e.aux)[(int64_t)i * e.ld_aux + j]);
   } else if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
-    float pre = (float)((const TA*)e.aux)[(int64_t)i * e.ld_aux + j];
-    v *= (EPI == EPI_GELU_BWD) ? gelu_erf_grad(pre) : quick_gelu_grad(pre);
+    v *= (float)((const TA*)e.aux)[(int64_t)i * e.ld_aux + j];
     ((TO*)e.C)[(int64_t)i * e.ldc + j] = (TO)v;
   } else if constexpr (EPI == EPI_PATCH) {
     int b = i / e.n_patch, p = i - b * e.n_patch;
@@ -398,6 +573,10 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
     for (int a = 0; a < C::AI; ++a)
 #pragma unroll
       for (int b = 0; b < C::AJ; ++b) asm volatile("" ::"v"(acc[a][b]));
+    return;
+  }
+  if (!(e.dbg & 8)) {  // row-contiguous epilogue through LDS (dbg bit 8: the fragment-layout one, for timing)
+    epilogue_staged<C, EPI, TO, TA>(e, acc, smem, i0, j0, wi, wj, lane, M, N, z);
     return;
   }
   // epilogue: acc[a][b] holds C[i][j..j+3] with i = lane&15, j = 4*(lane>>4)
@@ -747,17 +926,19 @@ static int r_chunk_for(int R, int split, int bk) {
 template <class C, int PL, int QL, int EPI, typename TO, typename TA>
 static int launch_big(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
                       const Epi& e, hipStream_t s) {
+  constexpr int lds = C::LDS > EpiLds<C, TO>::BYTES ? C::LDS : EpiLds<C, TO>::BYTES;
+  static_assert(lds <= 163840, "LDS");
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)big::gemm_kernel<C, PL, QL, EPI, TO, TA>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+                              hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     attr = true;
   }
   if (R % C::BK) return (int)hipErrorInvalidValue;
   const int r_chunk = r_chunk_for(R, split, 64);  // one chunking for every variant (wgrad counts slabs)
   const int nz = (R + r_chunk - 1) / r_chunk;
   dim3 grid(((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN) * nz);
-  hipLaunchKernelGGL((big::gemm_kernel<C, PL, QL, EPI, TO, TA>), grid, dim3(C::THREADS), C::LDS, s,
+  hipLaunchKernelGGL((big::gemm_kernel<C, PL, QL, EPI, TO, TA>), grid, dim3(C::THREADS), lds, s,
                      (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, r_chunk, e);
   VIT_CHECK_LAUNCH();
   return 0;
@@ -873,7 +1054,7 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
 }
 
 // F.linear forward: Y[M,N] = X[M,K] W[N,K]^T + b with a fused epilogue
-//   epi = EPI_STORE (Y out_dtype), EPI_BIAS_GELU / EPI_BIAS_QGELU (Y = pre, act_out = act),
+//   epi = EPI_STORE (Y out_dtype), EPI_BIAS_GELU / EPI_BIAS_QGELU (Y = act'(pre), act_out = act(pre)),
 //   EPI_RESID (Y f32 = resid + X W^T + b; Y may alias resid).
 int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const void* X, int64_t ldx,
                    const void* W, const float* bias, void* Y, int64_t ldy, const void* resid,
@@ -883,7 +1064,8 @@ int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const
   return gemm_any(epi, dtype, out_dtype, LAY_RC, LAY_RC, M, N, K, X, ldx, W, K, 1, e, (hipStream_t)stream);
 }
 
-// Linear input gradient: dX[M,K] = dY[M,N] W[N,K]  (epi EPI_STORE or *_GELU_BWD with pre [M,K]).
+// Linear input gradient: dX[M,K] = dY[M,N] W[N,K]  (epi EPI_STORE or *_GELU_BWD: times the
+// act'(pre) [M,K] the forward epilogue saved).
 // dbias (optional, [K] f32) = column sums of dX as written by the epilogue (the bias
 // gradient of the Linear whose output gradient dX is, e.g. fc1's from fc2's dgrad with
 // the GELU' epilogue); needs `partial` >= vit_linear_dgrad_partial_floats(M, K).

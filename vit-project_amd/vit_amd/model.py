@@ -216,7 +216,9 @@ class _BlockFn(torch.autograd.Function):
         o = torch.empty(M, D, dtype=T, device=dev)
         lse = torch.empty(B * H * N, dtype=f32, device=dev)
         xm, xo = torch.empty(M, D, dtype=f32, device=dev), torch.empty(M, D, dtype=f32, device=dev)
-        pre, act = torch.empty(M, F, dtype=T, device=dev), torch.empty(M, F, dtype=T, device=dev)
+        # fc1's epilogue writes act = GELU(pre) for fc2 and dact = GELU'(pre) for the backward
+        # (the erf is evaluated once; the fc2 dgrad epilogue is then a multiply)
+        dact, act = torch.empty(M, F, dtype=T, device=dev), torch.empty(M, F, dtype=T, device=dev)
         Wqkv, Wproj, W1, W2 = _wt(qkvw, T), _wt(projw, T), _wt(fc1w, T), _wt(fc2w, T)
         causal = bool(cfg.get("causal", False))
 
@@ -229,7 +231,7 @@ class _BlockFn(torch.autograd.Function):
             ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N], causal=causal)
             ops.linear_fwd(o[sl], Wproj, projb.detach(), epi=L.EPI_RESID, resid=x2[sl], out=xm[sl])
             ops.layer_norm_fwd(xm[sl], n2w.detach(), n2b.detach(), eps, T, out=h2[sl], mean=m2[sl], rstd=r2[sl])
-            ops.linear_fwd(h2[sl], W1, fc1b.detach(), epi=act_epi, out=pre[sl], act_out=act[sl])
+            ops.linear_fwd(h2[sl], W1, fc1b.detach(), epi=act_epi, out=dact[sl], act_out=act[sl])
             ops.linear_fwd(act[sl], W2, fc2b.detach(), epi=L.EPI_RESID, resid=xm[sl], out=xo[sl])
 
         side = _Side(dev)
@@ -242,7 +244,7 @@ class _BlockFn(torch.autograd.Function):
             side.join()
         else:
             chain(0, B)
-        ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, pre, act)
+        ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act)
         ctx.params = (n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.wops = (Wqkv, Wproj, W1, W2)
         ctx.meta = (B, N, D, H, T, cfg.get("compact_np", 0), cfg["quick_gelu"], causal)
@@ -250,7 +252,7 @@ class _BlockFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dxo):
-        x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, pre, act = ctx.saved_tensors
+        x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act = ctx.saved_tensors
         n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b = ctx.params
         Wqkv, Wproj, W1, W2 = ctx.wops
         B, N, D, H, T, compact_np, qg, causal = ctx.meta
@@ -282,7 +284,7 @@ class _BlockFn(torch.autograd.Function):
             side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g[11]))
         dx = None
         if need_mlp_in:
-            dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=pre, dbias=g[10])
+            dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=dact, dbias=g[10])
             if ng[9]:
                 side.run(lambda: ops.linear_wgrad(dpre, h2, out=g[9]))
         if any(ng[0:9]):

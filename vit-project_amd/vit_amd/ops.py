@@ -40,7 +40,8 @@ def _s(t: torch.Tensor) -> int:
 # ----------------------------------------------------------------------------
 
 def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, resid=None, act_out=None):
-    """y = epi(x @ w^T + bias).  x2d [M,K] (row stride x2d.stride(0)), w [N,K] contiguous."""
+    """y = epi(x @ w^T + bias).  x2d [M,K] (row stride x2d.stride(0)), w [N,K] contiguous.
+    EPI_BIAS_GELU / EPI_BIAS_QGELU return (act'(pre), act(pre)) with pre = x @ w^T + bias."""
     L.require_gpu(x2d)
     M, K = x2d.shape
     N = w.shape[0]
@@ -64,7 +65,8 @@ def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, res
 
 
 def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, out=None, dbias=None):
-    """dx = dy @ w  (dy [M,N], w [N,K]) with optional activation-grad epilogue on pre [M,K];
+    """dx = dy @ w  (dy [M,N], w [N,K]); with EPI_GELU_BWD / EPI_QGELU_BWD times ``pre`` [M,K] =
+    the act'(pre) the forward's BIAS_GELU epilogue saved;
     dbias [K] (optional) receives the column sums of dx (fused into the GEMM epilogue)."""
     M, N = dy2d.shape
     K = w.shape[1]
