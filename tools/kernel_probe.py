@@ -35,6 +35,17 @@ for _ in range(reps):
             lw, lb = torch.ones(D, device=dev), torch.zeros(D, device=dev)
             y = torch.empty(M, D, device=dev, dtype=bf)
         ops.layer_norm_fwd(xf, lw, lb, 1e-6, bf, out=y)
+    elif which in ("sdpa_fwd", "sdpa_bwd"):  # bs=256 ViT-B/16 attention (12 heads, N=197)
+        if _ == 0:
+            B, H, N = 256, 12, 197
+            qkv = torch.randn(M, 3 * D, device=dev).to(bf)
+            o, lse = ops.sdpa_fwd(qkv, B, H, N)
+            do = torch.randn(M, D, device=dev).to(bf)
+            dq = torch.empty_like(qkv)
+        if which == "sdpa_fwd":
+            ops.sdpa_fwd(qkv, B, H, N, o=o)
+        else:
+            ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dqkv=dq)
     elif which == "dgrad_fc1":
         ops.linear_dgrad(dy, w, out_dtype=bf)
 torch.cuda.synchronize()

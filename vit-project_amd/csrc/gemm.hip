@@ -575,9 +575,13 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
       for (int b = 0; b < C::AJ; ++b) asm volatile("" ::"v"(acc[a][b]));
     return;
   }
-  if (!(e.dbg & 8)) {  // row-contiguous epilogue through LDS (dbg bit 8: the fragment-layout one, for timing)
-    epilogue_staged<C, EPI, TO, TA>(e, acc, smem, i0, j0, wi, wj, lane, M, N, z);
-    return;
+  // bf16 outputs: row-contiguous epilogue through LDS (16-B stores; dbg bit 8 forces the
+  // fragment-layout one, for timing).  f32 fragments already store 16 B per lane.
+  if constexpr (sizeof(TO) == 2) {
+    if (!(e.dbg & 8)) {
+      epilogue_staged<C, EPI, TO, TA>(e, acc, smem, i0, j0, wi, wj, lane, M, N, z);
+      return;
+    }
   }
   // epilogue: acc[a][b] holds C[i][j..j+3] with i = lane&15, j = 4*(lane>>4)
   f32x4 cs[C::AJ];
@@ -789,6 +793,8 @@ using V3 = Cfg<128, 256, 32, 2, 2, 3, false, 2>;  //  72 KiB, 2 WG/CU (4 waves o
 using V4 = Cfg<256, 128, 32, 4, 2, 4, false, 4>;  //  96 KiB, 1 WG/CU, 4-deep ring
 }  // namespace big
 
+#include "pgemm.inc"
+
 // ----------------------------------------------------------------------------
 // Generic strided kernel: any M, N, R; f32 or bf16 inputs; fp32 FMA.
 //   P(i,r) = P[i*sPi + r*sPr], Q(j,r) = Q[j*sQj + r*sQr]
@@ -907,14 +913,15 @@ static int g_variant = -1;  // -1: per-shape choice; 1, 2, 5: force big::V<n>, 8
 static int g_dbg = 0;
 
 // per-shape choice among the kept configurations (sweep on MI355X, bs=256 ViT-B/16 shapes)
-static int pick_variant(int pl, int ql, int M, int N, int R, int split) {
+static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool pers_ok) {
   int v;
   if (g_variant >= 0) v = g_variant % 100;
   else if (split > 1 || (pl == LAY_CR && ql == LAY_CR)) v = 8;           // wgrad: ping-pong 256x256
   else if (pl == LAY_RC && ql == LAY_RC) v = (N >= 1536 || R >= 1536) ? 5 : 2;  // forward
   else v = (N <= 1024 && R <= 1024) ? 1 : 3;                              // dgrad
   (void)M;
-  if ((v == 2 || v == 5) && R % 64) v = 1;                                  // BK = 64 configurations need 64-row chunks
+  if ((v == 2 || v == 5 || v == 10) && R % 64) v = 1;                       // BK = 64 configurations need 64-row chunks
+  if (v == 10 && (!pers_ok || split > 1)) v = 1;
   return v;
 }
 
@@ -964,10 +971,49 @@ static int launch_pp(const void* P, int64_t ldp, const void* Q, int64_t ldq, int
   return 0;
 }
 
+static int num_cus() {
+  static int n = 0;
+  if (n <= 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  }
+  return n;
+}
+static unsigned g_pers_slot = 0;  // scheduler-counter slot of the next persistent launch (round robin)
+
+template <int PL, int QL, int EPI, typename TO, typename TA>
+static int launch_pers(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, const Epi& e,
+                       hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)pers::gemm_kernel<PL, QL, EPI, TO, TA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, pers::C::LDS);
+    attr = true;
+  }
+  if (R % pers::C::BK) return (int)hipErrorInvalidValue;
+  const int tiles = ((M + pers::C::BM - 1) / pers::C::BM) * ((N + pers::C::BN - 1) / pers::C::BN);
+  const int grid = tiles < num_cus() ? tiles : num_cus();
+  const int slot = (int)(g_pers_slot++ % pers::NSLOT);
+  hipLaunchKernelGGL((pers::gemm_kernel<PL, QL, EPI, TO, TA>), dim3(grid), dim3(pers::C::THREADS), pers::C::LDS, s,
+                     (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, e, slot);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
 template <int PL, int QL, int EPI, typename TO, typename TA>
 static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R,
                        int split, const Epi& e, hipStream_t s) {
-  switch (pick_variant(PL, QL, M, N, R, split)) {
+  constexpr bool pers_ok = PL == LAY_RC && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU ||
+                                            EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
+  const int v = pick_variant(PL, QL, M, N, R, split, pers_ok);
+  if constexpr (pers_ok) {
+    // the persistent kernel's buffer-descriptor stores need full column tiles and 32-bit offsets
+    if (v == 10 && N % pers::C::BN == 0 && (int64_t)M * e.ldc * (int64_t)sizeof(TO) < ((int64_t)1 << 31))
+      return launch_pers<PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, e, s);
+    if (v == 10) return launch_big<big::V1, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+  }
+  switch (v) {
     case 2: return launch_big<big::V2, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 5: return launch_big<big::V5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 3: return launch_big<big::V3, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
@@ -992,6 +1038,18 @@ static int launch_gen(const void* P, int64_t sPi, int64_t sPr, const void* Q, in
   return 0;
 }
 
+// (layout, epilogue, output type) combinations the model uses get MFMA kernels; any other
+// goes to the generic kernel (keeps the instantiation count, and the build time, down).
+template <int PL, int QL, int EPI, typename TO> constexpr bool fast_combo() {
+  constexpr bool f32o = std::is_same<TO, float>::value;
+  if (PL == LAY_RC && QL == LAY_RC)  // forward
+    return EPI == EPI_STORE || ((EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) && !f32o) ||
+           ((EPI == EPI_RESID || EPI == EPI_PATCH) && f32o);
+  if (PL == LAY_RC && QL == LAY_CR) return EPI == EPI_STORE || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD;  // dgrad
+  if (PL == LAY_CR && QL == LAY_CR) return EPI == EPI_STORE && f32o;  // wgrad (f32 slabs)
+  return EPI == EPI_STORE;                                           // CR x RC (raw vit_gemm)
+}
+
 // One dispatcher for all layouts/epilogues.  out_dtype selects TO; for the
 // *_BWD epilogues the pre-activation has the input dtype.
 template <int EPI>
@@ -1001,8 +1059,11 @@ static int gemm_dispatch(int dtype, int out_dtype, int pl, int ql, int M, int N,
   if (M <= 0 || N <= 0) return 0;
   if (allow_fast && fast_ok(dtype, pl, ql, M, N, R, P, Q, ldp, ldq) && (e.ldc % 4 == 0)) {
 #define FAST(PLx, QLx)                                                                                  \
-    if (out_dtype == VIT_F32) return launch_fast<PLx, QLx, EPI, float, bf16>(P, ldp, Q, ldq, M, N, R, split, e, s); \
-    else return launch_fast<PLx, QLx, EPI, bf16, bf16>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    if (out_dtype == VIT_F32) {                                                                         \
+      if constexpr (fast_combo<PLx, QLx, EPI, float>()) return launch_fast<PLx, QLx, EPI, float, bf16>(P, ldp, Q, ldq, M, N, R, split, e, s); \
+    } else {                                                                                            \
+      if constexpr (fast_combo<PLx, QLx, EPI, bf16>()) return launch_fast<PLx, QLx, EPI, bf16, bf16>(P, ldp, Q, ldq, M, N, R, split, e, s); \
+    }
     if (pl == LAY_RC && ql == LAY_RC) { FAST(LAY_RC, LAY_RC) }
     if (pl == LAY_RC && ql == LAY_CR) { FAST(LAY_RC, LAY_CR) }
     if (pl == LAY_CR && ql == LAY_CR) { FAST(LAY_CR, LAY_CR) }
