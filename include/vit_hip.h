@@ -58,7 +58,10 @@ int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const
  * fc1.bias from fc2's dgrad), fused into the epilogue; partial >= vit_linear_dgrad_partial_floats. */
 int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, const void* dY, int64_t lddy,
                      const void* W, void* dX, int64_t lddx, const void* pre, float* dbias, float* partial,
-                     int64_t partial_floats, void* stream);
+                     int64_t partial_floats, int defer_reduce, void* stream);
+/* defer_reduce = 1: dbias is not written; `partial` keeps its [ceil(M/64)][K] column-sum
+ * partials for the caller to reduce with vit_colreduce (e.g. on another stream, off the
+ * input-gradient chain). */
 int vit_linear_dgrad_partial_floats(int M, int K);
 
 /* F.linear weight gradient dW (f32) = dY^T X, split-K over rows with fp32 slabs
@@ -95,7 +98,10 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
                        const void* dy, int64_t lddy, const float* w, const float* mean, const float* rstd,
                        const float* dres, int64_t ldres, float* dx, int64_t lddx, void* dx_copy, int64_t ld_copy,
                        int dtype_copy, int compact_np, float* dgamma, float* dbeta, float* dsum, float* partial,
-                       int64_t partial_floats, void* stream);
+                       int64_t partial_floats, int defer_reduce, void* stream);
+/* defer_reduce = 1: dgamma / dbeta / dsum are not written; `partial` keeps their
+ * [ceil(rows/64)][D] partials at float offsets 0, nblk*D, 2*nblk*D (followed by the
+ * vit_colreduce scratch) for the caller to reduce with vit_colreduce. */
 int vit_layer_norm_bwd_partial_floats(int rows, int D);
 
 /* F.scaled_dot_product_attention(q,k,v) (timm Attention, head_dim 64, N <= 288) reading q/k/v in

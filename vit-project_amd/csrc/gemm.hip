@@ -1137,7 +1137,7 @@ int vit_linear_dgrad_partial_floats(int M, int K) {
 
 int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, const void* dY, int64_t lddy,
                      const void* W, void* dX, int64_t lddx, const void* pre, float* dbias, float* partial,
-                     int64_t partial_floats, void* stream) {
+                     int64_t partial_floats, int defer_reduce, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   Epi e = make_epi();
   e.C = dX; e.ldc = lddx; e.aux = pre; e.ld_aux = lddx;
@@ -1158,6 +1158,7 @@ int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, con
                          lddx, M, K, 64, partial);
     VIT_CHECK_LAUNCH();
   }
+  if (defer_reduce) return 0;  // the caller reduces the partials (vit_colreduce)
   launch_colreduce(partial, rows, K, dbias, 0, s, partial + (int64_t)rows * K);
   VIT_CHECK_LAUNCH();
   return 0;

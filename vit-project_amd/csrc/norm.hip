@@ -248,7 +248,7 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
                        const void* dy, int64_t lddy, const float* w, const float* mean, const float* rstd,
                        const float* dres, int64_t ldres, float* dx, int64_t lddx, void* dx_copy, int64_t ld_copy,
                        int dtype_copy, int compact_np, float* dgamma, float* dbeta, float* dsum, float* partial,
-                       int64_t partial_floats, void* stream) {
+                       int64_t partial_floats, int defer_reduce, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (rows <= 0) return 0;
   if (D > 64 * LN_SMAX) return (int)hipErrorInvalidValue;
@@ -273,6 +273,7 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
   else { LB(bf16, float) }
 #undef LB
   VIT_CHECK_LAUNCH();
+  if (defer_reduce) return 0;  // the caller reduces the partials (vit_colreduce)
   if (dgamma) {
     launch_colreduce(pg, nblk, D, dgamma, 0, s, scratch);
     launch_colreduce(pb, nblk, D, dbeta, 0, s, scratch);

@@ -28,7 +28,7 @@ SIGNATURES = {
     "vit_gemm_variant": [i32],
     "vit_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, vp],
     "vit_linear_fwd": [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, i64, vp, vp, vp],
-    "vit_linear_dgrad": [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, i64, vp, vp, vp, i64, vp],
+    "vit_linear_dgrad": [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, i64, vp, vp, vp, i64, i32, vp],
     "vit_linear_dgrad_partial_floats": [i32, i32],
     "vit_colreduce": [vp, i32, i32, vp, i32, vp, vp],
     "vit_linear_wgrad": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i32, vp, i64, vp],
@@ -36,7 +36,7 @@ SIGNATURES = {
     "vit_patch_embed_fwd": [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
     "vit_layer_norm_fwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, f32, vp],
     "vit_layer_norm_bwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, i32,
-                           i32, vp, vp, vp, vp, i64, vp],
+                           i32, vp, vp, vp, vp, i64, i32, vp],
     "vit_layer_norm_bwd_partial_floats": [i32, i32],
     "vit_sdpa_fwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, f32, i32, vp],
     "vit_sdpa_bwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, f32, i32, vp, vp, i64, vp],

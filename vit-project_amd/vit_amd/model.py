@@ -284,7 +284,7 @@ class _BlockFn(torch.autograd.Function):
             side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g[11]))
         dx = None
         if need_mlp_in:
-            dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=dact, dbias=g[10])
+            dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=dact, dbias=g[10], reduce_on=side)
             if ng[9]:
                 side.run(lambda: ops.linear_wgrad(dpre, h2, out=g[9]))
         if any(ng[0:9]):
@@ -293,7 +293,7 @@ class _BlockFn(torch.autograd.Function):
             dxm_c = dxm if T == torch.float32 else torch.empty(M, D, dtype=T, device=dev)
             ops.layer_norm_bwd(xm, D, dh2, n2w.detach(), m2, r2, dxm, D, M, dres=dxo, ldres=D,
                                dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=g[7], dbeta=g[8],
-                               dsum=g[6])
+                               dsum=g[6], reduce_on=side)
             # attention
             if ng[5]:
                 side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5]))
@@ -312,7 +312,8 @@ class _BlockFn(torch.autograd.Function):
                 # column sums of dx = the upstream block's fc2.bias gradient (not needed below the first block)
                 dsum = None if (compact_np or not ng[0]) else torch.empty(D, dtype=torch.float32, device=dev)
                 ops.layer_norm_bwd(x2, D, dh1, n1w.detach(), m1, r1, dx, D, M, dres=dxm, ldres=D, dx_copy=dx_c,
-                                   ld_copy=D, compact_np=compact_np, dgamma=g[1], dbeta=g[2], dsum=dsum)
+                                   ld_copy=D, compact_np=compact_np, dgamma=g[1], dbeta=g[2], dsum=dsum,
+                                   reduce_on=side)
                 if ng[0] and (dx_c is not None or dsum is not None):
                     _put_copy(dx, dx_c, dsum)
         side.join()

@@ -35,6 +35,13 @@ def _s(t: torch.Tensor) -> int:
     return L.stream_ptr(t.device)
 
 
+def _keep(t: torch.Tensor):
+    """t is read by work queued on the current stream after its producer's stream moves on:
+    the caching allocator must not hand its memory out again before that work ran."""
+    if t.is_cuda:
+        t.record_stream(torch.cuda.current_stream(t.device))
+
+
 # ----------------------------------------------------------------------------
 # GEMMs
 # ----------------------------------------------------------------------------
@@ -64,10 +71,12 @@ def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, res
     return (out, act_out) if epi in (L.EPI_BIAS_GELU, L.EPI_BIAS_QGELU) else out
 
 
-def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, out=None, dbias=None):
+def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, out=None, dbias=None, reduce_on=None):
     """dx = dy @ w  (dy [M,N], w [N,K]); with EPI_GELU_BWD / EPI_QGELU_BWD times ``pre`` [M,K] =
     the act'(pre) the forward's BIAS_GELU epilogue saved;
-    dbias [K] (optional) receives the column sums of dx (fused into the GEMM epilogue)."""
+    dbias [K] (optional) receives the column sums of dx (fused into the GEMM epilogue).
+    ``reduce_on`` (an object with ``.run(fn)``, e.g. the model's side stream): the final
+    reduction of those column sums is issued through it instead of inline."""
     M, N = dy2d.shape
     K = w.shape[1]
     assert w.shape[0] == N and w.dtype == dy2d.dtype and dy2d.stride(1) == 1
@@ -76,12 +85,22 @@ def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, ou
     if pre is not None:
         assert pre.stride(0) == out.stride(0)
     part, nfl = None, 0
+    defer = dbias is not None and reduce_on is not None
     if dbias is not None:
         assert dbias.dtype == torch.float32 and dbias.is_contiguous() and dbias.numel() == K
         nfl = L.lib().vit_linear_dgrad_partial_floats(M, K)
-        part = workspace("dgrad_bias", nfl * 4, dy2d.device)
+        # a deferred reduction reads the partials later on another stream: own buffer
+        part = (torch.empty(nfl, dtype=torch.float32, device=dy2d.device) if defer
+                else workspace("dgrad_bias", nfl * 4, dy2d.device))
     call("vit_linear_dgrad", L.dt(dy2d), L.dt(out), epi, M, N, K, ptr(dy2d), dy2d.stride(0), ptr(w), ptr(out),
-         out.stride(0), ptr(pre), ptr(dbias), ptr(part), nfl, _s(dy2d))
+         out.stride(0), ptr(pre), ptr(dbias), ptr(part), nfl, int(defer), _s(dy2d))
+    if defer:
+        rows = (M + 63) // 64
+
+        def finish():
+            _keep(part)
+            colreduce(part, rows, K, dbias, scratch=part[rows * K:])
+        reduce_on.run(finish)
     return out
 
 
@@ -146,18 +165,35 @@ def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, nee
 
 
 def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0, dx_copy=None, ld_copy=0,
-                   compact_np=0, dgamma=None, dbeta=None, dsum=None, ws="ln_partial"):
-    """dsum [D] (optional) receives the column sums of dx (a Linear bias gradient)."""
+                   compact_np=0, dgamma=None, dbeta=None, dsum=None, ws="ln_partial", reduce_on=None):
+    """dsum [D] (optional) receives the column sums of dx (a Linear bias gradient).
+    ``reduce_on`` (an object with ``.run(fn)``): the dgamma / dbeta / dsum reductions of the
+    per-64-row partials are issued through it (e.g. on the side stream) instead of inline."""
     D = w.numel()
     part = None
     nfl = 0
-    if dgamma is not None or dsum is not None:
+    want = dgamma is not None or dsum is not None
+    defer = want and reduce_on is not None
+    if want:
         nfl = L.lib().vit_layer_norm_bwd_partial_floats(rows, D)
-        part = workspace(ws, nfl * 4, x.device)
+        part = (torch.empty(nfl, dtype=torch.float32, device=x.device) if defer
+                else workspace(ws, nfl * 4, x.device))
     call("vit_layer_norm_bwd", L.dt(x), L.dt(dy), rows, D, ptr(x), ldx, ptr(dy), dy.stride(0), ptr(w), ptr(mean),
          ptr(rstd), ptr(dres), ldres, ptr(dx), lddx, ptr(dx_copy), ld_copy,
          L.dt(dx_copy) if dx_copy is not None else L.BF16, compact_np, ptr(dgamma), ptr(dbeta), ptr(dsum), ptr(part),
-         nfl, _s(x))
+         nfl, int(defer), _s(x))
+    if defer:
+        nb = (rows + 63) // 64
+        sc = part[3 * nb * D:]
+
+        def finish():
+            _keep(part)
+            if dgamma is not None:
+                colreduce(part[:nb * D], nb, D, dgamma, scratch=sc)
+                colreduce(part[nb * D:2 * nb * D], nb, D, dbeta, scratch=sc)
+            if dsum is not None:
+                colreduce(part[2 * nb * D:3 * nb * D], nb, D, dsum, scratch=sc)
+        reduce_on.run(finish)
 
 
 # ----------------------------------------------------------------------------
