@@ -22,6 +22,7 @@ epilogue, bias grads into column-sum kernels.
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -63,6 +64,12 @@ def _put_copy(g: torch.Tensor, copy, dsum=None):
 # joins (main waits on side) before returning its gradients.  Capturable.
 _SIDE = {}
 _OVERLAP = [True]
+# forward half-batch chains: join the two streams after every block ("block") or once after
+# the block stack ("end", default)
+_FWD_JOIN = [os.environ.get("VIT_FWD_JOIN", "end")]
+# block backward: join the side stream (weight/bias gradients) at the end of every block
+# ("block") or once, in the patch embedding's backward ("end": flat-gradient runs only)
+_BWD_JOIN = [os.environ.get("VIT_BWD_JOIN", "end")]
 
 
 def set_wgrad_overlap(enable: bool):
@@ -116,6 +123,10 @@ class _Shadowed:
                 p._vit_shadow_version = p._version
 
 
+def cfg_defer_bwd(ctx) -> bool:
+    return getattr(ctx, "defer_bwd", False)
+
+
 def _gout(p: nn.Parameter) -> torch.Tensor:
     """Where a parameter's gradient is written: its slice of the model's flat
     gradient buffer (fixed addresses: one all-reduce, a static optimizer table,
@@ -167,6 +178,7 @@ class _PatchEmbedFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dx):
+        _Side(dx.device).join()  # weight-gradient work the blocks left on the side stream
         (U,) = ctx.saved_tensors
         B, npatch, D, wshape, T = ctx.meta
         dx = dx.contiguous()
@@ -241,13 +253,17 @@ class _BlockFn(torch.autograd.Function):
             hb = B // 2
             side.run(lambda: chain(hb, B))
             chain(0, hb)
-            side.join()
+            # each half only feeds the same half of the next block: a stack of blocks joins
+            # once after its last block (cfg "defer_join", ViT._tokens) instead of per block
+            if not cfg.get("defer_join"):
+                side.join()
         else:
             chain(0, B)
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act)
         ctx.params = (n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.wops = (Wqkv, Wproj, W1, W2)
         ctx.meta = (B, N, D, H, T, cfg.get("compact_np", 0), cfg["quick_gelu"], causal)
+        ctx.defer_bwd = bool(cfg.get("defer_bwd_join"))
         return xo.reshape(B, N, D)
 
     @staticmethod
@@ -276,8 +292,8 @@ class _BlockFn(torch.autograd.Function):
         # gradient: fc2.bias from the upstream LayerNorm backward (side channel), fc1.bias
         # from the GELU' dgrad epilogue, proj.bias from LN2 backward, qkv.bias from SDPA backward.
         if ng[12]:
-            if dxo_sum is not None:
-                ops.colreduce(dxo_sum, 1, D, g[12])
+            if dxo_sum is not None:  # the upstream LayerNorm backward's column sums (side stream)
+                side.run(lambda: ops.colreduce(dxo_sum, 1, D, g[12]))
             else:
                 ops.colsum(dxo_c, out=g[12])
         if ng[11]:
@@ -316,7 +332,8 @@ class _BlockFn(torch.autograd.Function):
                                    reduce_on=side)
                 if ng[0] and (dx_c is not None or dsum is not None):
                     _put_copy(dx, dx_c, dsum)
-        side.join()
+        if not cfg_defer_bwd(ctx):
+            side.join()
         return (dx.reshape(B, N, D) if (ng[0] and dx is not None) else None, *g[1:], None)
 
 
@@ -508,9 +525,17 @@ class VisionTransformer(nn.Module):
         x = _PatchEmbedFn.apply(x.to(torch.float32), pe.proj.weight, pe.proj.bias, self.cls_token, self.pos_embed,
                                 cfg)
         n = len(self.blocks)
+        cfg["defer_join"] = _FWD_JOIN[0] == "end"
+        # gradients in the flat buffer are only read after backward (optimizer / allreduce_flat),
+        # so the blocks may leave their weight-gradient work pending until the patch embedding
+        # (and no .grad is accumulated into: AccumulateGrad would add on the main stream)
+        cfg["defer_bwd_join"] = (_BWD_JOIN[0] == "end" and getattr(self, "flat_grad", None) is not None
+                                 and torch.is_grad_enabled() and all(p.grad is None for p in self.parameters()))
         for i, blk in enumerate(self.blocks):
             bcfg = cfg if i != 0 else dict(cfg, compact_np=pe.num_patches)
             x = _BlockFn.apply(x, *blk.block_params(), bcfg)
+        if cfg["defer_join"]:
+            _Side(x.device).join()  # the side stream's half-batch chain of the last block
         return x
 
     def forward_features(self, x):
