@@ -103,6 +103,7 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
  * [ceil(rows/64)][D] partials at float offsets 0, nblk*D, 2*nblk*D (followed by the
  * vit_colreduce scratch) for the caller to reduce with vit_colreduce. */
 int vit_layer_norm_bwd_partial_floats(int rows, int D);
+int vit_layer_norm_bwd_blocks(int rows); /* partial rows: the [nblk][D] partial blocks' nblk */
 
 /* F.scaled_dot_product_attention(q,k,v) (timm Attention, head_dim 64, N <= 288) reading q/k/v in
  * place from the qkv GEMM output; lse [B*H*N] f32.  causal = 1 masks key > query: the CLIP text

@@ -98,6 +98,14 @@ def main():
     y = torch.empty(M, D, device=dev, dtype=bf)
     t = timeit(lambda: ops.layer_norm_fwd(x, w, bb, 1e-6, bf, out=y), a.reps)
     print(json.dumps({"name": "ln_fwd", "ms": round(t * 1e3, 4), "GBps": round(M * D * 6 / t / 1e9, 1)}))
+    # block backward's LayerNorm: x f32, dy bf16, dres f32 in; dx f32 + bf16 copy out; dgamma/dbeta/dsum
+    _, mean, rstd = ops.layer_norm_fwd(x, w, bb, 1e-6, bf, out=y)
+    dres, dxo = torch.randn(M, D, device=dev), torch.empty(M, D, device=dev)
+    dxc = torch.empty(M, D, device=dev, dtype=bf)
+    gg, gb, gs = (torch.empty(D, device=dev) for _ in range(3))
+    t = timeit(lambda: ops.layer_norm_bwd(x, D, y, w, mean, rstd, dxo, D, M, dres=dres, ldres=D, dx_copy=dxc,
+                                          ld_copy=D, dgamma=gg, dbeta=gb, dsum=gs), a.reps)
+    print(json.dumps({"name": "ln_bwd", "ms": round(t * 1e3, 4), "GBps": round(M * D * 20 / t / 1e9, 1)}))
 
 
 def torch_ref(a):

@@ -9,9 +9,20 @@
 // scalar kernel (NV = 0) covers any other D (test configs).
 #include "common.hpp"
 #include "reduce.hpp"
+#include <stdlib.h>
 
 constexpr int LN_WAVES = 4;   // rows per block in the forward (one per wave)
 constexpr int LN_SMAX = 32;   // scalar path: D <= 64*32
+// rows per backward block (one partial row each); VIT_LN_BWD_ROWS overrides (tuning)
+static int ln_bwd_rows() {
+  static int r = 0;
+  if (r <= 0) {
+    const char* s = getenv("VIT_LN_BWD_ROWS");
+    r = s ? atoi(s) : 32;
+    if (r < 4) r = 32;
+  }
+  return r;
+}
 
 template <typename T> __device__ __forceinline__ f32x4 ld4(const T* p);
 template <> __device__ __forceinline__ f32x4 ld4<float>(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
@@ -161,6 +172,28 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     }
   }
   if (!part_g && !part_s) return;
+  if constexpr (NV > 0) {
+    // per-block partials of dgamma / dbeta / dsum: one LDS round (one barrier pair) per
+    // quantity, the four waves each summing a quarter of the slots
+    __shared__ float redv[LN_WAVES][NP][64];
+    auto flush = [&](const float (&p)[NP], float* out) {
+#pragma unroll
+      for (int k = 0; k < NP; ++k) redv[wv][k][lane] = p[k];
+      __syncthreads();
+#pragma unroll
+      for (int k = wv; k < NP; k += LN_WAVES) {
+        const float v = (redv[0][k][lane] + redv[1][k][lane]) + (redv[2][k][lane] + redv[3][k][lane]);
+        out[(int64_t)blockIdx.x * D + col4(lane, k >> 2) + (k & 3)] = v;
+      }
+      __syncthreads();
+    };
+    if (part_g) {
+      flush(pg, part_g);
+      flush(pb, part_b);
+    }
+    if (part_s) flush(ps, part_s);
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < NP; ++k) {
     const int c = NV > 0 ? col4(lane, k >> 2) + (k & 3) : k * 64 + lane;
@@ -239,8 +272,10 @@ int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x,
 // dgamma/dbeta and dsum = column sums of dx (the bias gradient of the Linear that
 // produced the LayerNorm's residual input) may each be null; `partial` must hold
 // vit_layer_norm_bwd_partial_floats(rows, D) floats when any of them is requested.
+int vit_layer_norm_bwd_blocks(int rows) { return (rows + ln_bwd_rows() - 1) / ln_bwd_rows(); }
+
 int vit_layer_norm_bwd_partial_floats(int rows, int D) {
-  const int nblk = (rows + 63) / 64;
+  const int nblk = vit_layer_norm_bwd_blocks(rows);
   return (int)(3 * (int64_t)nblk * D + colreduce_scratch_floats(nblk, D));
 }
 
@@ -252,8 +287,8 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
   hipStream_t s = (hipStream_t)stream;
   if (rows <= 0) return 0;
   if (D > 64 * LN_SMAX) return (int)hipErrorInvalidValue;
-  const int rows_per = 64;
-  const int nblk = (rows + rows_per - 1) / rows_per;
+  const int rows_per = ln_bwd_rows();
+  const int nblk = vit_layer_norm_bwd_blocks(rows);
   const bool want = dgamma != nullptr || dsum != nullptr;
   if (want && (partial == nullptr || partial_floats < vit_layer_norm_bwd_partial_floats(rows, D)))
     return (int)hipErrorInvalidValue;

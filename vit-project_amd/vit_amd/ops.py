@@ -190,7 +190,7 @@ def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0
          L.dt(dx_copy) if dx_copy is not None else L.BF16, compact_np, ptr(dgamma), ptr(dbeta), ptr(dsum), ptr(part),
          nfl, int(defer), _s(x))
     if defer:
-        nb = (rows + 63) // 64
+        nb = L.lib().vit_layer_norm_bwd_blocks(rows)
         sc = part[3 * nb * D:]
 
         def finish():
