@@ -913,12 +913,12 @@ static int g_variant = -1;  // -1: per-shape choice; 1, 2, 5: force big::V<n>, 8
 static int g_dbg = 0;
 
 // per-shape choice among the kept configurations (sweep on MI355X, bs=256 ViT-B/16 shapes)
-static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool pers_ok) {
+static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool pers_ok, bool act_bwd) {
   int v;
   if (g_variant >= 0) v = g_variant % 100;
   else if (split > 1 || (pl == LAY_CR && ql == LAY_CR)) v = 8;           // wgrad: ping-pong 256x256
   else if (pl == LAY_RC && ql == LAY_RC) v = (N >= 1536 || R >= 1536) ? 5 : 2;  // forward
-  else v = (N <= 1024 && R <= 1024) ? 1 : 3;                              // dgrad
+  else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;                // dgrad (GELU' epilogue: V1, 2 WG/CU)
   (void)M;
   if ((v == 2 || v == 5 || v == 10) && R % 64) v = 1;                       // BK = 64 configurations need 64-row chunks
   if (v == 10 && (!pers_ok || split > 1)) v = 1;
@@ -1006,7 +1006,7 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
                        int split, const Epi& e, hipStream_t s) {
   constexpr bool pers_ok = PL == LAY_RC && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU ||
                                             EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
-  const int v = pick_variant(PL, QL, M, N, R, split, pers_ok);
+  const int v = pick_variant(PL, QL, M, N, R, split, pers_ok, EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
   if constexpr (pers_ok) {
     // the persistent kernel's buffer-descriptor stores need full column tiles and 32-bit offsets
     if (v == 10 && N % pers::C::BN == 0 && (int64_t)M * e.ldc * (int64_t)sizeof(TO) < ((int64_t)1 << 31))
