@@ -208,3 +208,46 @@ def test_clip_l14_step_runs():
     assert tuple(pred.shape) == (4, 66) and torch.isfinite(pred).all() and torch.isfinite(loss)
     with_grad = [n for n, q in m.named_parameters() if q.grad is not None]
     assert len(with_grad) == 9 and all(n.rsplit(".", 1)[1] in ("m", "delta_D_A", "delta_D_B") for n in with_grad)
+
+
+@pytest.mark.gpu
+def test_sweep_condition_on_cliphba(tmp_path):
+    """vit_amd.sweep on the real CLIPHBA(ViT-L/14) + DoRA: a baseline epoch, then one perturbed
+    condition resumed from its files; the DoRA checkpoint keys are the reference's (NEWP:666-683)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import numpy as np
+    import vit_amd
+    from vit_amd import sweep as S
+
+    def make():
+        torch.manual_seed(0)
+        m = vit_amd.CLIPHBA(["c%d" % i for i in range(66)], "ViT-L/14", pos_embedding=True)
+        vit_amd.apply_dora_to_ViT(m, n_vision_layers=2, n_transformer_layers=1, r=32)
+        vit_amd.switch_dora_layers(m, freeze_all=True, dora_state=True)
+        m = m.cuda()
+        return m, vit_amd.FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=3e-4)
+
+    g = torch.Generator().manual_seed(1)
+    dev = "cuda"
+    mk = lambda n: (torch.randn(n, 3, 224, 224, generator=g).to(dev), (torch.randn(n, 66, generator=g) + 2).to(dev))
+    a = np.random.default_rng(0).random((48, 48))
+    ref = (a + a.T) / 2
+    np.fill_diagonal(ref, 0)
+    data = dict(train=mk(16), test=mk(8), inference=torch.randn(48, 3, 224, 224, generator=g).to(dev),
+                reference_rdm=ref)
+    m, opt = make()
+    base = tmp_path / "base"
+    rows = S.train_condition(m, opt, vit_amd.mse_loss, data, epochs=1, training_run=1, perturb_length=0,
+                             perturb_type=None, batch_size=8, training_res_path=str(tmp_path / "b.csv"),
+                             dora_parameters_path=str(base / "dora"), random_state_path=str(base / "rs"),
+                             dataloader_generator=torch.Generator().manual_seed(0))
+    assert len(rows) == 1 and np.isfinite(rows[0][1]) and np.isfinite(rows[0][3])
+    sd = torch.load(str(base / "dora" / "epoch1_dora_params.pth"), weights_only=True)
+    assert sorted(sd) == sorted(f"{p}.{k}" for p in S.DORA_MODULES for k in ("m", "delta_D_A", "delta_D_B"))
+    done = S.run_sweep(make, vit_amd.mse_loss, data, [(2, 1)], perturb_type="label_shuffle",
+                       out_dir=str(tmp_path / "sw"), baseline_dora_path=str(base / "dora"),
+                       baseline_random_state_path=str(base / "rs"), epochs=2, batch_size=8)
+    with open(done[0][1]) as fh:
+        out = fh.read().splitlines()
+    assert out[0].split(",") == S.CSV_HEADERS and out[1].split(",")[0] == "2" and out[1].split(",")[6] == "True"
