@@ -232,6 +232,81 @@ template <class C, typename TO> struct EpiLds {
   static_assert(C::THREADS % CPR == 0 && C::WM % RL == 0 && 64 % RL == 0, "epilogue sweep shape");
 };
 
+// bf16 epilogue straight from the MFMA fragments with 16-B stores (no LDS round trip).
+// A lane holds C[i][4g..4g+3] of each 16-column fragment (g = lane >> 4).  For a fragment
+// pair (b, b+1), one v_permlane16_swap per dword (vdst = fragment b, src = fragment b+1)
+// trades lane rows g=1 / g=3 of b with rows g=0 / g=2 of b+1, after which every lane holds 8
+// consecutive columns of the pair: g=0 cols 0-7, g=2 8-15, g=1 16-23, g=3 24-31 -- one
+// dwordx4 store instead of two dwordx2 (the fragment-layout store tail is issue-bound).
+// Needs N % 32 == 0 (whole 8-column groups).
+template <int EPI, typename TO, typename TA>
+__device__ __forceinline__ f32x4 epi_val(const Epi& e, int i, int j, f32x4 v, bool ok, f32x4& o0, f32x4& o1) {
+  if (e.bias && ok) v += *reinterpret_cast<const f32x4*>(e.bias + j);
+  if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const float pr = (float)(TO)v[t];  // pre-activation rounded to the storage type
+      float ga, gd;
+      if constexpr (EPI == EPI_BIAS_GELU) gelu_fast_both(pr, ga, gd);
+      else quick_gelu_both(pr, ga, gd);
+      o0[t] = gd;
+      o1[t] = ga;
+    }
+  } else if constexpr (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) {
+    v *= ok ? load4<TA>((const TA*)e.aux + (int64_t)i * e.ld_aux + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+    o0 = v;
+  } else {  // EPI_STORE
+    o0 = v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void store_pair_bf16(void* base, int64_t ldc, int i, int col, const f32x4& x,
+                                                const f32x4& y, bool ok) {
+  const bf16x4 px = {(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
+  const bf16x4 py = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
+  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x2 ux = __builtin_bit_cast(u32x2, px), uy = __builtin_bit_cast(u32x2, py);
+  const auto r0 = __builtin_amdgcn_permlane16_swap(ux[0], uy[0], false, false);
+  const auto r1 = __builtin_amdgcn_permlane16_swap(ux[1], uy[1], false, false);
+  if (ok) *reinterpret_cast<u32x4*>((bf16*)base + (int64_t)i * ldc + col) = u32x4{r0[0], r1[0], r0[1], r1[1]};
+}
+
+template <class C, int EPI, typename TO, typename TA>
+__device__ __forceinline__ void epilogue_swap(const Epi& e, const f32x4 (&acc)[C::AI][C::AJ], int i0, int j0, int wi,
+                                              int wj, int lane, int M, int N) {
+  static_assert(C::AJ % 2 == 0, "fragment pairs");
+  constexpr bool two = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU;
+  const int g = lane >> 4;
+  const int colsel = (g & 1) * 16 + (g >> 1) * 8;
+  f32x4 cs[C::AJ];
+#pragma unroll
+  for (int b = 0; b < C::AJ; ++b) cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int a = 0; a < C::AI; ++a) {
+    const int i = i0 + wi * C::WM + a * 16 + (lane & 15);
+    const bool row_ok = i < M;
+#pragma unroll
+    for (int b = 0; b < C::AJ; b += 2) {
+      const int jp = j0 + wj * C::WN + b * 16;
+      const int ja = jp + 4 * g, jb = jp + 16 + 4 * g;
+      const bool oka = row_ok && ja < N, okb = row_ok && jb < N;
+      f32x4 xa, ya, xb, yb;
+      const f32x4 va = epi_val<EPI, TO, TA>(e, i, ja, acc[a][b], oka, xa, ya);
+      const f32x4 vb = epi_val<EPI, TO, TA>(e, i, jb, acc[a][b + 1], okb, xb, yb);
+      if (e.csum) {
+        if (oka) cs[b] += va;
+        if (okb) cs[b + 1] += vb;
+      }
+      const bool ok = row_ok && jp + colsel < N;
+      store_pair_bf16(e.C, e.ldc, i, jp + colsel, xa, xb, ok);
+      if constexpr (two) store_pair_bf16(e.aux_out, e.ldc, i, jp + colsel, ya, yb, ok);
+    }
+    if (e.csum && (a & 3) == 3) csum_flush<C::AJ>(e, cs, i0 + wi * C::WM + (a - 3) * 16, M, N, j0 + wj * C::WN, lane);
+  }
+}
+
 // Staged epilogue: for each band of WM rows (the waves of one wi), those waves
 // write their f32 accumulators to LDS, then the whole workgroup sweeps the band
 // row-contiguously through epi_vec.  Column sums (fused bias gradients) are
@@ -577,6 +652,17 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
   }
   // bf16 outputs: row-contiguous epilogue through LDS (16-B stores; dbg bit 8 forces the
   // fragment-layout one, for timing).  f32 fragments already store 16 B per lane.
+  // bf16 outputs: plain stores of the smaller tiles go out as fragment pairs widened to 16-B
+  // stores by permlane16_swap (N % 32 == 0; +2-5 % over staging on the N = 768 outputs); the
+  // 256x256 tile and the GELU / GELU' epilogues are faster through the row-contiguous LDS
+  // staging (tools/bench_kernels.py --sweep: v vs 6400 + v).  Timing flags: dbg 64 forces the
+  // staged epilogue, dbg 8 the plain fragment-layout one below (8-B stores).
+  if constexpr (sizeof(TO) == 2 && EPI == EPI_STORE && C::BM * C::BN < 256 * 256) {
+    if (!(e.dbg & (8 | 64)) && N % 32 == 0) {
+      epilogue_swap<C, EPI, TO, TA>(e, acc, i0, j0, wi, wj, lane, M, N);
+      return;
+    }
+  }
   if constexpr (sizeof(TO) == 2) {
     if (!(e.dbg & 8)) {
       epilogue_staged<C, EPI, TO, TA>(e, acc, smem, i0, j0, wi, wj, lane, M, N, z);
