@@ -101,10 +101,18 @@ def main():
     x = torch.randn(B, 3, 224, 224, device=dev)
     y = torch.randint(0, 1000, (B,), device=dev)
 
+    # world > 1: gradients averaged block by block during the backward (RCCL beside compute);
+    # VIT_DDP_OVERLAP=0 falls back to bucketed all-reduces after the backward
+    reducer = None
+    if world > 1 and os.environ.get("VIT_DDP_OVERLAP", "1") != "0":
+        reducer = parallel.OverlappedGradReduce(model)
+
     def step():
         loss = vit_amd.cross_entropy(model(x), y)
         loss.backward()
-        if world > 1:
+        if reducer is not None:
+            reducer.finish()
+        elif world > 1:
             parallel.allreduce_flat(flat, bucket_mb=64.0)
         opt.step()
         opt.zero_grad(set_to_none=True)

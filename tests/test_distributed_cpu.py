@@ -47,6 +47,57 @@ def test_allreduce_flat_world2():
         assert err < 1e-5, (rank, err)
 
 
+class _FlatModel:
+    def __init__(self, flat):
+        self.flat_grad = flat
+        self.hook = None
+
+    def set_grad_ready_hook(self, fn):
+        self.hook = fn
+
+
+def _worker_overlap(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from vit_amd import parallel
+    parallel.init_from_env(backend="gloo")
+    n = 100_003
+    flat = torch.randn(n, generator=torch.Generator().manual_seed(rank))
+    expect = sum(torch.randn(n, generator=torch.Generator().manual_seed(k)) for k in range(world)) / world
+    m = _FlatModel(flat)
+    red = parallel.OverlappedGradReduce(m)
+    # block spans reported during "backward" (out of order, leaving gaps at both ends and between)
+    m.hook(50_000, 70_000)
+    m.hook(10_000, 30_000)
+    m.hook(30_000, 50_000)
+    red.finish()
+    err = float((flat - expect).abs().max())
+    # second step reuses the reducer: everything reduced again in finish() alone
+    flat.copy_(torch.full((n,), float(rank)))
+    red.finish()
+    err2 = float((flat - (world - 1) / 2).abs().max())
+    q.put((rank, err, err2))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlapped_grad_reduce_world2():
+    """OverlappedGradReduce: block spans reduced as they are reported, the rest in finish()."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_overlap, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, err, err2 in res:
+        assert err < 1e-5 and err2 < 1e-6, (rank, err, err2)
+
+
 def test_shard_conditions_partition_and_chains():
     from vit_amd import parallel
     conds = parallel.length_sweep_conditions()

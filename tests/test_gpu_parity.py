@@ -236,3 +236,57 @@ def test_reference_training_loop_unchanged(golden_dir):
             assert _rel(v, fx["params_after"][k]) < 1e-3, k
     finally:
         dist.destroy_process_group()
+
+
+def _ddp_worker(rank, world, port, q):
+    import os as _os
+    _os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                       LOCAL_RANK="0")
+    import torch.distributed as dist
+    import vit_amd
+    from vit_amd import parallel
+    dist.init_process_group("gloo", init_method="env://", rank=rank, world_size=world)
+    torch.cuda.set_device(0)
+    cfg = R.VIT_B16
+    p = R.init_params(cfg, seed=5, random_affine=True)
+    x, y = _inputs(cfg, 4, 100 + rank)  # different images per rank
+    m = _model(cfg, p, torch.bfloat16)
+    flat = m.use_flat_grads(True)
+    xd, yd = x.to(DEV), y.to(DEV)
+    vit_amd.cross_entropy(m(xd), yd).backward()  # local gradients
+    torch.cuda.synchronize()
+    local = flat.detach().cpu().clone()
+    m.zero_grad(set_to_none=True)
+    red = parallel.OverlappedGradReduce(m)
+    vit_amd.cross_entropy(m(xd), yd).backward()  # block spans all-reduced during the backward
+    ncov = len(red.covered)
+    red.finish()
+    torch.cuda.synchronize()
+    q.put((rank, local, flat.detach().cpu().clone(), ncov))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_ddp_overlapped_allreduce_two_ranks():
+    """The N>1 bench path: OverlappedGradReduce hooked into the block backward (spans reduced
+    from the side stream while the backward continues) gives the rank-average of the local
+    flat gradients.  Two processes on the one GPU, gloo over CUDA tensors (RCCL needs one GPU
+    per rank); the stream ordering under test is the same."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_ddp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for pr in procs:
+        pr.start()
+    res = sorted([q.get(timeout=300) for _ in range(2)], key=lambda t: t[0])
+    for pr in procs:
+        pr.join(timeout=120)
+        assert pr.exitcode == 0
+    mean = (res[0][1] + res[1][1]) / 2
+    for rank, local, reduced, ncov in res:
+        assert ncov == 12  # one span per block
+        assert (reduced - mean).abs().max().item() <= 1e-6 * mean.abs().max().item() + 1e-7, rank

@@ -264,6 +264,8 @@ class _BlockFn(torch.autograd.Function):
         ctx.wops = (Wqkv, Wproj, W1, W2)
         ctx.meta = (B, N, D, H, T, cfg.get("compact_np", 0), cfg["quick_gelu"], causal)
         ctx.defer_bwd = bool(cfg.get("defer_bwd_join"))
+        ctx.grad_hook = cfg.get("grad_hook")
+        ctx.flat_span = cfg.get("flat_span")
         return xo.reshape(B, N, D)
 
     @staticmethod
@@ -332,6 +334,9 @@ class _BlockFn(torch.autograd.Function):
                                    reduce_on=side)
                 if ng[0] and (dx_c is not None or dsum is not None):
                     _put_copy(dx, dx_c, dsum)
+        if ctx.grad_hook is not None and all(ng[1:13]):
+            # every gradient of this block is enqueued (side stream, after the main stream's work)
+            side.run(lambda: ctx.grad_hook(*ctx.flat_span))
         if not cfg_defer_bwd(ctx):
             side.join()
         return (dx.reshape(B, N, D) if (ng[0] and dx is not None) else None, *g[1:], None)
@@ -510,7 +515,22 @@ class VisionTransformer(nn.Module):
             self.flat_grad_slices.append((off, p.numel()))
             off += p.numel()
         self.flat_grad = flat
+        # each block's parameters are contiguous in the buffer: its span for an overlapped all-reduce
+        ends = {}
+        off = 0
+        for p in order:
+            ends[id(p)] = (off, off + p.numel())
+            off += p.numel()
+        for blk in self.blocks:
+            spans = [ends[id(p)] for p in blk.block_params()]
+            blk._flat_span = (min(s for s, _ in spans), max(e for _, e in spans))
         return flat
+
+    def set_grad_ready_hook(self, fn):
+        """fn(lo, hi) is called by each block's backward once the block's gradients (the flat
+        buffer's [lo, hi)) are enqueued, on the stream they were enqueued on
+        (vit_amd.parallel.OverlappedGradReduce)."""
+        self._grad_hook = fn
 
     def shadow_params(self):
         self._ensure_shadows()
@@ -529,10 +549,15 @@ class VisionTransformer(nn.Module):
         # gradients in the flat buffer are only read after backward (optimizer / allreduce_flat),
         # so the blocks may leave their weight-gradient work pending until the patch embedding
         # (and no .grad is accumulated into: AccumulateGrad would add on the main stream)
+        # (and the patch embedding's backward -- the join point -- must run: its weight trains)
         cfg["defer_bwd_join"] = (_BWD_JOIN[0] == "end" and getattr(self, "flat_grad", None) is not None
-                                 and torch.is_grad_enabled() and all(p.grad is None for p in self.parameters()))
+                                 and torch.is_grad_enabled() and pe.proj.weight.requires_grad
+                                 and all(p.grad is None for p in self.parameters()))
+        hook = getattr(self, "_grad_hook", None) if cfg["defer_bwd_join"] else None
         for i, blk in enumerate(self.blocks):
             bcfg = cfg if i != 0 else dict(cfg, compact_np=pe.num_patches)
+            if hook is not None:
+                bcfg = dict(bcfg, grad_hook=hook, flat_span=blk._flat_span)
             x = _BlockFn.apply(x, *blk.block_params(), bcfg)
         if cfg["defer_join"]:
             _Side(x.device).join()  # the side stream's half-batch chain of the last block
