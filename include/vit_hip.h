@@ -75,6 +75,11 @@ int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, f
 /* out[N] (+)= sum_z part[z][:] over S partial rows (second stage of fused bias gradients);
  * scratch optional (>= ceil(S/64)*N floats, faster for S > 64). */
 int vit_colreduce(const float* part, int S, int N, float* out, int accumulate, float* scratch, void* stream);
+/* nq (1..3) stacked [S][N] partial matrices (part + q*S*N) reduced into out0..out2 with one
+ * launch per stage (the LayerNorm backward's dgamma | dbeta | dsum partials); scratch optional
+ * (>= nq*ceil(S/64)*N floats). */
+int vit_colreduce_multi(const float* part, int nq, int S, int N, float* out0, float* out1, float* out2,
+                        int accumulate, float* scratch, void* stream);
 
 /* timm PatchEmbed Conv2d(3,768,16,16) as GEMM over unfolded patches, writing
  * rows b*(np+1)+1+p of the f32 token stream with pos_embed added (VIT:139). */

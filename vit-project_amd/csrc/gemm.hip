@@ -1259,6 +1259,16 @@ int vit_colreduce(const float* part, int S, int N, float* out, int accumulate, f
   return 0;
 }
 
+// nq (<= 3) stacked [S][N] partial matrices reduced in one launch per stage into out0..out2.
+int vit_colreduce_multi(const float* part, int nq, int S, int N, float* out0, float* out1, float* out2,
+                        int accumulate, float* scratch, void* stream) {
+  if (nq < 1 || nq > 3 || S <= 0 || N <= 0) return nq == 0 ? 0 : (int)hipErrorInvalidValue;
+  float* outs[3] = {out0, out1, out2};
+  launch_colreduce_multi(part, nq, S, N, outs, accumulate, (hipStream_t)stream, scratch);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
 // Linear weight gradient: dW[N,K] (f32) = dY[M,N]^T X[M,K], split over M into
 // `split` fp32 slabs in `workspace` (>= split*N*K*4 bytes) then reduced.
 int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t lddy, const void* X,

@@ -115,8 +115,14 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
     int64_t orow = row;
     const bool keep = (dxc != nullptr) && copy_row(row, compact_np, orow);
     if constexpr (NV > 0) {
-      f32x4 xh[NV], g[NV];
+      f32x4 xh[NV], g[NV], rv[NV];
       float s1 = 0.f, s2 = 0.f;
+      // the residual gradient is loaded with x and dy, so a row costs one memory round trip
+      if (dres) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          rv[k] = *reinterpret_cast<const f32x4*>(dres + (int64_t)row * ldres + col4(lane, k));
+      }
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         int c = col4(lane, k);
@@ -139,7 +145,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
         f32x4 o;
 #pragma unroll
         for (int t = 0; t < 4; ++t) o[t] = rs * (g[k][t] - s1 - xh[k][t] * s2);
-        if (dres) o += *reinterpret_cast<const f32x4*>(dres + (int64_t)row * ldres + c);
+        if (dres) o += rv[k];
 #pragma unroll
         for (int t = 0; t < 4; ++t) ps[k * 4 + t] += o[t];
         *reinterpret_cast<f32x4*>(dxr + c) = o;
@@ -276,7 +282,7 @@ int vit_layer_norm_bwd_blocks(int rows) { return (rows + ln_bwd_rows() - 1) / ln
 
 int vit_layer_norm_bwd_partial_floats(int rows, int D) {
   const int nblk = vit_layer_norm_bwd_blocks(rows);
-  return (int)(3 * (int64_t)nblk * D + colreduce_scratch_floats(nblk, D));
+  return (int)(3 * (int64_t)nblk * D + 3 * colreduce_scratch_floats(nblk, D));
 }
 
 int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x, int64_t ldx,
@@ -309,11 +315,12 @@ int vit_layer_norm_bwd(int dtype_x, int dtype_dy, int rows, int D, const void* x
 #undef LB
   VIT_CHECK_LAUNCH();
   if (defer_reduce) return 0;  // the caller reduces the partials (vit_colreduce)
-  if (dgamma) {
-    launch_colreduce(pg, nblk, D, dgamma, 0, s, scratch);
-    launch_colreduce(pb, nblk, D, dbeta, 0, s, scratch);
+  {
+    // the [pg | pb | ps] partial matrices are stacked: one two-stage reduction for all
+    float* outs[3] = {dgamma, dbeta, dsum};
+    if (dgamma) launch_colreduce_multi(pg, dsum ? 3 : 2, nblk, D, outs, 0, s, scratch);
+    else if (dsum) launch_colreduce_multi(ps, 1, nblk, D, outs + 2, 0, s, scratch);
   }
-  if (dsum) launch_colreduce(ps, nblk, D, dsum, 0, s, scratch);
   VIT_CHECK_LAUNCH();
   return 0;
 }

@@ -6,10 +6,16 @@
 #include "common.hpp"
 
 namespace {
-// block (x, y): columns x*64 .. x*64+63, partial rows [y*rows_per, min(S, (y+1)*rows_per))
-__global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict__ part, int S, int N, int rows_per,
-                                                         float* __restrict__ out, int64_t ldo, int accumulate) {
+struct ColOut {
+  float* p[3];
+};
+
+// block (x, y, z): columns x*64 .. x*64+63 of partial matrix z (part + z*zin), partial rows
+// [y*rows_per, min(S, (y+1)*rows_per)) -> out.p[z][y*ldo + column]
+__global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict__ part, int64_t zin, int S, int N,
+                                                         int rows_per, ColOut out, int64_t ldo, int accumulate) {
   __shared__ float red[16][65];
+  part += blockIdx.z * zin;
   const int c = threadIdx.x & 63, sl = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + c;
   const int z0 = blockIdx.y * rows_per, z1 = min(S, z0 + rows_per);
@@ -30,25 +36,42 @@ __global__ __launch_bounds__(1024) void colreduce_kernel(const float* __restrict
     float s = 0.f;
 #pragma unroll
     for (int k = 0; k < 16; ++k) s += red[k][c];
-    float* o = out + (int64_t)blockIdx.y * ldo + j;
+    float* o = out.p[blockIdx.z] + (int64_t)blockIdx.y * ldo + j;
     *o = accumulate ? *o + s : s;
   }
 }
 
-// out[j] (+)= sum_z part[z][j].  With `scratch` (>= ceil(S/64)*N floats) and S > 64
-// the rows are first reduced in 64-row groups by ceil(S/64) x ceil(N/64) blocks
-// (enough workgroups to hide load latency), then the group sums in a second pass.
-inline void launch_colreduce(const float* part, int S, int N, float* out, int accumulate, hipStream_t s,
-                             float* scratch = nullptr) {
+inline int64_t colreduce_scratch_floats(int S, int N) { return S > 64 ? (int64_t)((S + 63) / 64) * N : 0; }
+
+// out[q][j] (+)= sum_z part[q][z][j] for nq (<= 3) stacked [S][N] partial matrices, in one
+// launch per stage.  With `scratch` (>= nq * colreduce_scratch_floats(S, N) floats) and
+// S > 64 the rows are first reduced in 64-row groups by ceil(S/64) x ceil(N/64) blocks per
+// matrix (enough workgroups to hide load latency), then the group sums in a second pass.
+inline void launch_colreduce_multi(const float* part, int nq, int S, int N, float* const* outs, int accumulate,
+                                   hipStream_t s, float* scratch = nullptr) {
+  if (part == nullptr || nq < 1 || S <= 0 || N <= 0) return;
+  for (int q = 0; q < nq; ++q)
+    if (outs[q] == nullptr) return;
   const int nb = (N + 63) / 64;
+  ColOut o{};
+  for (int q = 0; q < nq; ++q) o.p[q] = outs[q];
   if (scratch != nullptr && S > 64) {
     const int G = (S + 63) / 64;
-    hipLaunchKernelGGL(colreduce_kernel, dim3(nb, G), dim3(1024), 0, s, part, S, N, 64, scratch, (int64_t)N, 0);
-    hipLaunchKernelGGL(colreduce_kernel, dim3(nb, 1), dim3(1024), 0, s, (const float*)scratch, G, N, G, out,
-                       (int64_t)0, accumulate);
+    ColOut sc{};
+    for (int q = 0; q < nq; ++q) sc.p[q] = scratch + (int64_t)q * G * N;
+    hipLaunchKernelGGL(colreduce_kernel, dim3(nb, G, nq), dim3(1024), 0, s, part, (int64_t)S * N, S, N, 64, sc,
+                       (int64_t)N, 0);
+    hipLaunchKernelGGL(colreduce_kernel, dim3(nb, 1, nq), dim3(1024), 0, s, (const float*)scratch, (int64_t)G * N, G,
+                       N, G, o, (int64_t)0, accumulate);
   } else {
-    hipLaunchKernelGGL(colreduce_kernel, dim3(nb, 1), dim3(1024), 0, s, part, S, N, S, out, (int64_t)0, accumulate);
+    hipLaunchKernelGGL(colreduce_kernel, dim3(nb, 1, nq), dim3(1024), 0, s, part, (int64_t)S * N, S, N, S, o,
+                       (int64_t)0, accumulate);
   }
 }
-inline int64_t colreduce_scratch_floats(int S, int N) { return S > 64 ? (int64_t)((S + 63) / 64) * N : 0; }
+
+// out[j] (+)= sum_z part[z][j] (scratch: >= colreduce_scratch_floats(S, N) floats).
+inline void launch_colreduce(const float* part, int S, int N, float* out, int accumulate, hipStream_t s,
+                             float* scratch = nullptr) {
+  launch_colreduce_multi(part, 1, S, N, &out, accumulate, s, scratch);
+}
 }  // namespace

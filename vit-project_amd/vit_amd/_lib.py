@@ -31,6 +31,7 @@ SIGNATURES = {
     "vit_linear_dgrad": [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, i64, vp, vp, vp, i64, i32, vp],
     "vit_linear_dgrad_partial_floats": [i32, i32],
     "vit_colreduce": [vp, i32, i32, vp, i32, vp, vp],
+    "vit_colreduce_multi": [vp, i32, i32, i32, vp, vp, vp, i32, vp, vp],
     "vit_linear_wgrad": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i32, vp, i64, vp],
     "vit_colsum": [i32, i32, i32, vp, i64, vp, vp, i64, i32, vp],
     "vit_patch_embed_fwd": [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],

@@ -171,6 +171,9 @@ def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, nee
     return out, mean, rstd
 
 
+_LN_MULTI = [os.environ.get("VIT_LN_MULTI", "1") != "0"]
+
+
 def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0, dx_copy=None, ld_copy=0,
                    compact_np=0, dgamma=None, dbeta=None, dsum=None, ws="ln_partial", reduce_on=None):
     """dsum [D] (optional) receives the column sums of dx (a Linear bias gradient).
@@ -195,11 +198,17 @@ def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0
 
         def finish():
             _keep(part)
-            if dgamma is not None:
-                colreduce(part[:nb * D], nb, D, dgamma, scratch=sc)
-                colreduce(part[nb * D:2 * nb * D], nb, D, dbeta, scratch=sc)
-            if dsum is not None:
-                colreduce(part[2 * nb * D:3 * nb * D], nb, D, dsum, scratch=sc)
+            # the [dgamma | dbeta | dsum] partials are stacked: one launch per reduction stage
+            if not _LN_MULTI[0]:
+                for q, o in enumerate((dgamma, dbeta, dsum)):
+                    if o is not None:
+                        colreduce(part[q * nb * D:(q + 1) * nb * D], nb, D, o, scratch=sc)
+            elif dgamma is not None:
+                call("vit_colreduce_multi", ptr(part), 3 if dsum is not None else 2, nb, D, ptr(dgamma),
+                     ptr(dbeta), ptr(dsum), 0, ptr(sc), _s(dgamma))
+            else:
+                call("vit_colreduce_multi", ptr(part[2 * nb * D:]), 1, nb, D, ptr(dsum), None, None, 0,
+                     ptr(sc), _s(dsum))
         reduce_on.run(finish)
 
 
