@@ -119,3 +119,76 @@ def test_bucket_bounds():
     from vit_amd import parallel
     assert parallel.bucket_bounds(10, 4) == [(0, 4), (4, 8), (8, 10)]
     assert parallel.bucket_bounds(86_567_656, 16 * 1024 * 1024)[-1][1] == 86_567_656
+
+
+class _FeatModel(torch.nn.Module):
+    """Stand-in with timm's forward_features surface: [B, 3, 4, 4] -> [B, 2, 16] (row 0 = CLS)."""
+    global_pool = "token"
+
+    def __init__(self):
+        super().__init__()
+        self.w = torch.nn.Parameter(torch.randn(48, 32, generator=torch.Generator().manual_seed(3)))
+
+    def forward_features(self, x):
+        return torch.tanh(x.flatten(1) @ self.w).reshape(x.shape[0], 2, 16)
+
+
+def _rsa_inputs():
+    import numpy as np
+    g = torch.Generator().manual_seed(7)
+    images = torch.randn(48, 3, 4, 4, generator=g)
+    a = np.random.default_rng(8).random((48, 48))
+    ref = (a + a.T) / 2
+    np.fill_diagonal(ref, 0.0)
+    return images, ref
+
+
+def _worker_rsa(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from vit_amd import parallel, rsa
+    parallel.init_from_env(backend="gloo")
+    images, ref = _rsa_inputs()
+    m = _FeatModel()
+    out = {o: rsa.compute_rsa_score(m, images, ref, world=world, rank=rank, order=o) for o in ("image", "reference")}
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 5])
+def test_compute_rsa_score_world(world):
+    """compute_rsa_score (MEAS:298-355) across gloo ranks: 'image' order equals the world-1 score;
+    'reference' order reproduces the reference's rank-concatenated rows, including
+    DistributedSampler's padding when 48 is not a multiple of the world size."""
+    import numpy as np
+    from vit_amd import rsa
+    images, ref = _rsa_inputs()
+    m = _FeatModel()
+    single = rsa.compute_rsa_score(m, images, ref)
+    emb = rsa.cls_embeddings(m, images)
+    quirk = [i for r in range(world) for i in rsa.sampler_indices(48, world, r)][:48]
+    want_ref = rsa.rsa(emb[quirk], ref)[:2]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_rsa, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(res[r]["image"] == (None, None) for r in range(1, world))
+    assert np.allclose(res[0]["image"], single, rtol=0, atol=1e-12)
+    assert np.allclose(res[0]["reference"], want_ref, rtol=0, atol=1e-12)
+    assert abs(res[0]["reference"][0] - single[0]) > 1e-6  # the quirk changes the score
+
+
+def test_sampler_indices_match_distributed_sampler():
+    from torch.utils.data import DistributedSampler
+    from vit_amd import rsa
+    for n, world in ((48, 2), (48, 5), (7, 3), (3, 8)):
+        for r in range(world):
+            s = DistributedSampler(range(n), num_replicas=world, rank=r, shuffle=False)
+            assert rsa.sampler_indices(n, world, r) == list(iter(s)), (n, world, r)

@@ -145,6 +145,9 @@ def test_rsa_rho_within_north_star(dtype):
     emb = vit_amd.rsa.cls_embeddings(m, imgs.to(DEV))
     rho, _, _ = vit_amd.rsa.rsa(emb, ref)
     assert abs(rho - rho_o) <= 0.005, (rho, rho_o)
+    # the MEAS:298 entry point (world 1) gives the same score
+    rho2, _ = vit_amd.rsa.compute_rsa_score(m, imgs.to(DEV), ref)
+    assert abs(rho2 - rho) <= 1e-6, (rho2, rho)
     if dtype == torch.float32:
         assert np.abs(emb - emb_o).max() <= 1e-3 * np.abs(emb_o).max()
 

@@ -78,3 +78,59 @@ def cls_embeddings(model, images, batch_size=8):
             else:
                 outs.append(f[:, 0].float().cpu())
     return torch.cat(outs).numpy()
+
+
+def sampler_indices(n: int, world: int, rank: int):
+    """Indices rank ``rank`` sees under DistributedSampler(shuffle=False, drop_last=False)
+    (torch/utils/data/distributed.py: pad to a multiple of ``world`` by repeating the head of
+    the index list, then take every ``world``-th index from ``rank``) -- the THINGS loader
+    of MEAS:298 at world > 1."""
+    idx = list(range(n))
+    total = -(-n // world) * world
+    pad = total - n
+    if pad:
+        idx += (idx * (-(-pad // n)))[:pad]
+    return idx[rank:total:world]
+
+
+def compute_rsa_score(model, images, reference_rdm, world: int = 1, rank: int = 0, batch_size: int = 8,
+                      order: str = "image", group=None):
+    """compute_rsa_score (MEAS:298-355) over ``world`` ranks: each rank embeds its
+    DistributedSampler share of the 48 images (``cls_embeddings``: forward_features[:, 0]),
+    the shares are all-gathered, and rank 0 returns (rho, p) of the model RDM against
+    ``reference_rdm``; other ranks return (None, None).
+
+    ``order`` settles SURVEY Appendix B Q3.  The reference concatenates the gathered shares
+    rank by rank and keeps the first 48 rows (MEAS:327-334), so at world > 1 its RDM rows are
+    [0, w, 2w, ..., 1, w+1, ...] against a reference RDM in image order.  ``"image"`` (default)
+    puts every row back at its image's index before the RDM; ``"reference"`` reproduces the
+    reference's concatenation order.  At world == 1 both are the reference's result."""
+    import torch
+    if order not in ("image", "reference"):
+        raise ValueError(f"order must be 'image' or 'reference', not {order!r}")
+    n = images.shape[0]
+    idx = sampler_indices(n, world, rank)
+    was_training = getattr(model, "training", False)
+    if hasattr(model, "eval"):
+        model.eval()
+    emb = cls_embeddings(model, images[idx], batch_size=batch_size)
+    if was_training:
+        model.train()
+    if world > 1:
+        import torch.distributed as dist
+        dev = images.device if images.device.type == "cuda" else torch.device("cpu")
+        t = torch.from_numpy(emb).to(dev)
+        parts = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(parts, t, group=group)
+        if rank != 0:
+            return None, None
+        rows = torch.cat(parts).cpu().numpy()
+        if order == "reference":
+            emb = rows[:n]
+        else:
+            where = [i for r in range(world) for i in sampler_indices(n, world, r)]
+            emb = np.empty((n, rows.shape[1]), dtype=rows.dtype)
+            for row, i in zip(rows, where):  # padded repeats carry the same image's row
+                emb[i] = row
+    rho, p, _ = rsa(emb, reference_rdm)
+    return rho, p
