@@ -169,6 +169,14 @@ int vit_rownorm_bwd(int n, int D, const float* x, const float* dy, const float* 
 int vit_mse_fwd(int n, const float* pred, const float* target, float* loss, void* stream);
 int vit_mse_bwd(int n, const float* pred, const float* target, const float* grad_loss, float* dpred, void* stream);
 
+/* ImageNet input transforms on the GPU (VIT:32-46, MEAS:152-158): RandomResizedCrop /
+ * Resize+CenterCrop with Pillow's 8-bit bilinear resampling (bit-exact), horizontal flip, ToTensor and
+ * Normalize, over a ragged batch of decoded RGB uint8 images in device memory.  params = device int64
+ * [B][12] (see image.hip); coeff_ws >= vit_image_coeff_bytes(B, S, kmax) bytes; out f32 [B][3][S][S]. */
+int vit_image_coeff_bytes(int B, int S, int kmax);
+int vit_image_transform(int B, int S, const uint8_t* src, const int64_t* params, int kmax, int max_rows,
+                        int* coeff_ws, uint8_t* tmp_ws, float* out, const float* norm6, void* stream);
+
 /* helpers */
 int vit_cast_f32_bf16(const float* x, void* y, int64_t n, void* stream);
 int vit_zero(void* p, int64_t bytes, void* stream);

@@ -10,10 +10,11 @@ from .dora import DoRALayer, dora_weight
 from . import rsa
 from . import clip
 from . import sweep
+from . import data
 from .clip import CLIPHBA, MSELoss, mse_loss, apply_dora_to_ViT, switch_dora_layers, count_trainable_parameters
 
 __all__ = ["VisionTransformer", "create_model", "cross_entropy", "set_wgrad_overlap", "FusedSGD", "FusedAdamW",
-           "CosineAnnealingLRWithWarmup", "DoRALayer", "dora_weight", "rsa", "clip", "CLIPHBA", "MSELoss",
+           "CosineAnnealingLRWithWarmup", "DoRALayer", "dora_weight", "rsa", "clip", "data", "CLIPHBA", "MSELoss",
            "mse_loss", "apply_dora_to_ViT", "switch_dora_layers", "count_trainable_parameters"]
 
 

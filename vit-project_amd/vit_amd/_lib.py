@@ -64,6 +64,8 @@ SIGNATURES = {
     "vit_rownorm_bwd": [i32, i32, vp, vp, vp, vp, vp, vp],
     "vit_mse_fwd": [i32, vp, vp, vp, vp],
     "vit_mse_bwd": [i32, vp, vp, vp, vp, vp],
+    "vit_image_coeff_bytes": [i32, i32, i32],
+    "vit_image_transform": [i32, i32, vp, vp, i32, i32, vp, vp, vp, vp, vp],
 }
 
 _lib = None
