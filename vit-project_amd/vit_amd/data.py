@@ -129,39 +129,50 @@ class GpuTransform:
             tmp += h * S * 3
         return tab
 
-    def __call__(self, images, generator=None, params=None) -> torch.Tensor:
-        S = self.size
+    def stage(self, images, generator=None, params=None):
+        """Host half: draw / validate the parameters, pack the uint8 images into one pinned buffer
+        and queue one host-to-device copy.  Returns the device-side batch for ``apply``."""
         shapes = [(int(im.shape[0]), int(im.shape[1])) for im in images]
         for im in images:
             if im.ndim != 3 or im.shape[2] != 3 or (im.dtype not in (np.uint8, torch.uint8)):
                 raise ValueError("images must be [H, W, 3] uint8")
         tab = self.plan(shapes, generator, params)
-        B = len(images)
-        out = torch.empty(B, 3, S, S, dtype=torch.float32, device=self.device)
-        if B == 0:
-            return out
-        L.require_gpu(out)
-        # one pinned staging buffer, one host-to-device copy for the whole batch
         total = int(sum(h * w * 3 for h, w in shapes))
-        host = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        host = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=torch.cuda.is_available())
         hv = host.numpy()
         for b, im in enumerate(images):
             a = im.numpy() if isinstance(im, torch.Tensor) else im
             n = a.shape[0] * a.shape[1] * 3
             hv[tab[b, 0]:tab[b, 0] + n] = np.ascontiguousarray(a).reshape(-1)
-        src = host.to(self.device, non_blocking=True)
-        dparams = torch.from_numpy(tab).to(self.device, non_blocking=True)
+        staged = {"tab": tab, "host": host}
+        if len(images):
+            staged["src"] = host.to(self.device, non_blocking=True)
+            staged["params"] = torch.from_numpy(tab).to(self.device, non_blocking=True)
+        return staged
+
+    def apply(self, staged) -> torch.Tensor:
+        """Device half: one ``vit_image_transform`` call over a staged batch -> f32 [B, 3, S, S]."""
+        S = self.size
+        tab = staged["tab"]
+        B = tab.shape[0]
+        out = torch.empty(B, 3, S, S, dtype=torch.float32, device=self.device)
+        if B == 0:
+            return out
+        L.require_gpu(out)
         kmax = max(max(_taps(int(t[5]), int(t[7])), _taps(int(t[4]), int(t[6]))) for t in tab)
         max_rows = int(tab[:, 4].max())
         tmp = torch.empty(int((tab[:, 4] * S * 3).sum()), dtype=torch.uint8, device=self.device)
         cws = torch.empty(L.lib().vit_image_coeff_bytes(B, S, kmax), dtype=torch.uint8, device=self.device)
-        call("vit_image_transform", B, S, ptr(src), ptr(dparams), kmax, max_rows, ptr(cws), ptr(tmp), ptr(out),
-             self.norm6.ctypes.data, L.stream_ptr(self.device))
+        call("vit_image_transform", B, S, ptr(staged["src"]), ptr(staged["params"]), kmax, max_rows, ptr(cws),
+             ptr(tmp), ptr(out), self.norm6.ctypes.data, L.stream_ptr(self.device))
         # the staging buffers are read by the queued kernels: keep them alive until they ran
         ev = torch.cuda.Event()
         ev.record()
-        self._inflight = (host, src, dparams, tmp, cws, ev)
+        self._inflight = (staged, tmp, cws, ev)
         return out
+
+    def __call__(self, images, generator=None, params=None) -> torch.Tensor:
+        return self.apply(self.stage(images, generator, params))
 
 
 def gaussian_noise(batch: torch.Tensor, epsilon: float = 0.1, generator=None) -> torch.Tensor:
