@@ -265,7 +265,8 @@ def _ddp_worker(rank, world, port, q):
     ncov = len(red.covered)
     red.finish()
     torch.cuda.synchronize()
-    q.put((rank, local, flat.detach().cpu().clone(), ncov))
+    # numpy (pickled by value): torch tensors would travel as shared-memory handles that die with this process
+    q.put((rank, local.numpy(), flat.detach().cpu().numpy(), ncov))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -292,4 +293,4 @@ def test_ddp_overlapped_allreduce_two_ranks():
     mean = (res[0][1] + res[1][1]) / 2
     for rank, local, reduced, ncov in res:
         assert ncov == 12  # one span per block
-        assert (reduced - mean).abs().max().item() <= 1e-6 * mean.abs().max().item() + 1e-7, rank
+        assert np.abs(reduced - mean).max() <= 1e-6 * np.abs(mean).max() + 1e-7, rank
