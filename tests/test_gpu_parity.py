@@ -294,3 +294,50 @@ def test_ddp_overlapped_allreduce_two_ranks():
     for rank, local, reduced, ncov in res:
         assert ncov == 12  # one span per block
         assert np.abs(reduced - mean).max() <= 1e-6 * np.abs(mean).max() + 1e-7, rank
+
+
+@pytest.mark.parametrize("train", [True, False])
+def test_two_stream_schedule_is_race_free(train):
+    """The bench path leaves side-stream work pending across blocks (forward half-batch chain
+    joined after the block stack, weight gradients joined in the patch embedding).  Tensors
+    that work reads are freed on the caller's stream before it runs; the allocator must not
+    hand them out again (record_stream).  Eager "end" joins must give bit-identical results to
+    the per-block-joined schedule, over several steps of allocator churn at bs=128."""
+    import vit_amd
+    from vit_amd import model as VM
+    cfg = R.VIT_B16
+    p = R.init_params(cfg, seed=21, random_affine=True)
+    x, y = _inputs(cfg, 128, 31)
+    xd, yd = x.to(DEV), y.to(DEV)
+    m = _model(cfg, p, torch.bfloat16)
+    if train:
+        flat = m.use_flat_grads(True)
+    else:
+        m.eval()
+
+    def run():
+        outs = []
+        for _ in range(3):
+            if train:
+                m.zero_grad(set_to_none=True)
+                vit_amd.cross_entropy(m(xd), yd).backward()
+                torch.cuda.synchronize()
+                outs.append(flat.detach().clone())
+            else:
+                with torch.no_grad():
+                    f = m.forward_features(xd)
+                    torch.cuda.synchronize()
+                    outs.append(f.float().clone())
+        return outs
+
+    saved = (VM._FWD_JOIN[0], VM._BWD_JOIN[0])
+    try:
+        VM._FWD_JOIN[0], VM._BWD_JOIN[0] = "block", "block"
+        ref = run()
+        VM._FWD_JOIN[0], VM._BWD_JOIN[0] = "end", "end"
+        got = run()
+    finally:
+        VM._FWD_JOIN[0], VM._BWD_JOIN[0] = saved
+    assert all(torch.equal(ref[0], r) for r in ref[1:]), "per-block joined schedule not deterministic"
+    for i, g in enumerate(got):
+        assert torch.equal(g, ref[0]), (i, (g - ref[0]).abs().max().item())

@@ -70,6 +70,8 @@ _FWD_JOIN = [os.environ.get("VIT_FWD_JOIN", "end")]
 # block backward: join the side stream (weight/bias gradients) at the end of every block
 # ("block") or once, in the patch embedding's backward ("end": flat-gradient runs only)
 _BWD_JOIN = [os.environ.get("VIT_BWD_JOIN", "end")]
+# record_stream on side-stream operands (VIT_RECORD_STREAMS=0 only to demonstrate the race it prevents)
+_RECORD = [os.environ.get("VIT_RECORD_STREAMS", "1") != "0"]
 
 
 def set_wgrad_overlap(enable: bool):
@@ -96,6 +98,15 @@ class _Side:
     def join(self):
         if self.on:
             self.main.wait_stream(self.side)
+
+    def guard(self, *ts):
+        """The side stream uses these tensors, possibly after their owner frees them on the
+        caller's stream (deferred joins): the caching allocator must wait for the side
+        stream's queued work before handing their memory out again."""
+        if self.on and _RECORD[0]:
+            for t in ts:
+                if t is not None and t.is_cuda:
+                    t.record_stream(self.side)
 
 
 class _Shadowed:
@@ -252,6 +263,7 @@ class _BlockFn(torch.autograd.Function):
             # overlap the other's MFMA main loops
             hb = B // 2
             side.run(lambda: chain(hb, B))
+            side.guard(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act, xo)
             chain(0, hb)
             # each half only feeds the same half of the next block: a stack of blocks joins
             # once after its last block (cfg "defer_join", ViT._tokens) instead of per block
@@ -286,6 +298,7 @@ class _BlockFn(torch.autograd.Function):
         need_h1 = any(ng[0:3])
         # gradient buffers are taken on the main stream (allocator ownership), filled on the side stream
         g = [None] * 13
+        dpre = dxm = dxm_c = do = dqkv = None
         for i, p in ((1, n1w), (2, n1b), (3, qkvw), (4, qkvb), (5, projw), (6, projb), (7, n2w), (8, n2b),
                      (9, fc1w), (10, fc1b), (11, fc2w), (12, fc2b)):
             if ng[i]:
@@ -334,6 +347,8 @@ class _BlockFn(torch.autograd.Function):
                                    reduce_on=side)
                 if ng[0] and (dx_c is not None or dsum is not None):
                     _put_copy(dx, dx_c, dsum)
+        side.guard(dxo, dxo_c, dxo_sum, x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act,
+                   *(v for v in (dpre, dxm, dxm_c, do, dqkv, dx) if v is not None), *(t for t in g if t is not None))
         if ctx.grad_hook is not None and all(ng[1:13]):
             # every gradient of this block is enqueued (side stream, after the main stream's work)
             side.run(lambda: ctx.grad_hook(*ctx.flat_span))

@@ -228,16 +228,17 @@ def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None, lse=None, causal=False):
     return o, lse
 
 
-def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None, causal=False):
-    """dbias [3*H*64] (optional) receives the column sums of dqkv (the qkv bias gradient)."""
+def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None, causal=False, ws=""):
+    """dbias [3*H*64] (optional) receives the column sums of dqkv (the qkv bias gradient).
+    ``ws``: workspace-name suffix (calls running concurrently on different streams need their own)."""
     if dqkv is None:
         dqkv = torch.empty_like(qkv2d)
     scale = 64 ** -0.5 if scale is None else scale
-    delta = workspace("sdpa_delta", B * H * N * 4, qkv2d.device)
+    delta = workspace("sdpa_delta" + ws, B * H * N * 4, qkv2d.device)
     part, nfl = None, 0
     if dbias is not None:
         nfl = L.lib().vit_sdpa_bwd_partial_floats(B, N, H * 64)
-        part = workspace("sdpa_bias", nfl * 4, qkv2d.device)
+        part = workspace("sdpa_bias" + ws, nfl * 4, qkv2d.device)
     call("vit_sdpa_bwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(do),
          do.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), ptr(delta), float(scale), int(causal), ptr(dbias),
          ptr(part), nfl, _s(qkv2d))
