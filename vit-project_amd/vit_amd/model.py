@@ -70,8 +70,9 @@ _FWD_JOIN = [os.environ.get("VIT_FWD_JOIN", "end")]
 # block backward: join the side stream (weight/bias gradients) at the end of every block
 # ("block") or once, in the patch embedding's backward ("end": flat-gradient runs only)
 _BWD_JOIN = [os.environ.get("VIT_BWD_JOIN", "end")]
-# record_stream on side-stream operands (VIT_RECORD_STREAMS=0 only to demonstrate the race it prevents)
-_RECORD = [os.environ.get("VIT_RECORD_STREAMS", "1") != "0"]
+# side-stream operands referenced until the next join (VIT_HOLD_REFS=0 only to demonstrate the race)
+_HOLD_REFS = [os.environ.get("VIT_HOLD_REFS", "1") != "0"]
+_HOLD = {}
 
 
 def set_wgrad_overlap(enable: bool):
@@ -98,15 +99,17 @@ class _Side:
     def join(self):
         if self.on:
             self.main.wait_stream(self.side)
+            # everything the side stream was given is ordered before the caller's later work now
+            _HOLD.pop(self.side, None)
 
     def guard(self, *ts):
-        """The side stream uses these tensors, possibly after their owner frees them on the
-        caller's stream (deferred joins): the caching allocator must wait for the side
-        stream's queued work before handing their memory out again."""
-        if self.on and _RECORD[0]:
-            for t in ts:
-                if t is not None and t.is_cuda:
-                    t.record_stream(self.side)
+        """The side stream uses these tensors, possibly after their owner drops them (deferred
+        joins leave its work queued across blocks): keep them referenced until the next join,
+        so the caching allocator cannot hand their memory to the caller's stream while that
+        work is pending.  (Not record_stream: its deferred-free events kept the pool from
+        reaching a steady state -- 15x slower steps.)"""
+        if self.on and _HOLD_REFS[0]:
+            _HOLD.setdefault(self.side, []).extend(t for t in ts if t is not None)
 
 
 class _Shadowed:
@@ -348,7 +351,9 @@ class _BlockFn(torch.autograd.Function):
                 if ng[0] and (dx_c is not None or dsum is not None):
                     _put_copy(dx, dx_c, dsum)
         side.guard(dxo, dxo_c, dxo_sum, x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act,
-                   *(v for v in (dpre, dxm, dxm_c, do, dqkv, dx) if v is not None), *(t for t in g if t is not None))
+                   *(v for v in (dpre, dxm, dxm_c, do, dqkv, dx) if v is not None))
+        # (not the gradients g: they alias the persistent flat buffer, and AccumulateGrad must be
+        # able to steal them -- an extra reference makes it copy before the side stream wrote them)
         if ctx.grad_hook is not None and all(ng[1:13]):
             # every gradient of this block is enqueued (side stream, after the main stream's work)
             side.run(lambda: ctx.grad_hook(*ctx.flat_span))
