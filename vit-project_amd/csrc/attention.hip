@@ -220,6 +220,47 @@ __device__ __forceinline__ void bias_flush(f32x4 (&c0)[4], f32x4 (*c1)[4], char*
   }
 }
 
+// Column sums of a 16-row fragment set c[dt][t] (rows = lane & 15, column dt*16 + 4g + t),
+// reduced over the 16 rows and kept compressed: lane l ends up owning column
+// (l15 >> 2) * 16 + 4g + (l15 & 3), one register instead of sixteen.
+__device__ __forceinline__ float colsum16(const f32x4 (&c)[4], int lane) {
+  const int l15 = lane & 15;
+  float own = 0.f;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float v = c[dt][t];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if (l15 == dt * 4 + t) own = v;
+    }
+  return own;
+}
+__device__ __forceinline__ int colsum16_col(int lane) {
+  const int l15 = lane & 15;
+  return (l15 >> 2) * 16 + 4 * (lane >> 4) + (l15 & 3);
+}
+// Flush per-lane compressed column sums (own[o] for output o) of the 8 waves into out.
+template <int NOUT>
+__device__ __forceinline__ void bias_flush_c(const float (&own)[NOUT], char* smem, float* out, int D) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* red = reinterpret_cast<float*>(smem);  // [NOUT][AT_WAVES][64]
+  __syncthreads();                              // every wave is done reading the LDS images
+#pragma unroll
+  for (int o = 0; o < NOUT; ++o) red[(o * AT_WAVES + wave) * 64 + colsum16_col(lane)] = own[o];
+  __syncthreads();
+  if (threadIdx.x < 64 * NOUT) {
+    const int o = threadIdx.x >> 6, d = threadIdx.x & 63;
+    float sum = 0.f;
+#pragma unroll
+    for (int w = 0; w < AT_WAVES; ++w) sum += red[(o * AT_WAVES + w) * 64 + d];
+    out[(NOUT == 1 ? 0 : (o + 1) * D) + d] = sum;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // bf16 backward, two kernels per (b, h) so each holds only half the head in LDS
 // (57 KiB -> two workgroups per CU):
@@ -344,9 +385,7 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
   const AtOffsets off(lane);
   __syncthreads();
   const float c2 = scale * LOG2E;
-  f32x4 csk[4], csv[4];  // column sums of dk, dv (qkv-bias gradient)
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) { csk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; csv[dt] = csk[dt]; }
+  float cs[2] = {0.f, 0.f};  // compressed column sums of dk, dv (qkv-bias gradient), colsum16 layout
   for (int kt = wave; kt < NT; kt += AT_WAVES) {
     const int key = kt * 16 + (lane & 15);
     const bool kvalid = key < N;
@@ -360,7 +399,7 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
     f32x4 dv[4], dk[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) { dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[dt] = dv[dt]; }
-#pragma unroll 1
+#pragma unroll 1  // unroll 2 spills ~300 VGPRs at the 128-register budget
     for (int qp = 0; qp < NT2; ++qp) {
       f32x4 p[2], ds[2];
 #pragma unroll
@@ -389,21 +428,27 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
         dk[dt] = mfma16(trf(Qimg, qp * 32, off.tr[dt]), dsf, dk[dt]);
       }
     }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dk[dt] = kvalid ? dk[dt] * scale : f32x4{0.f, 0.f, 0.f, 0.f};
+      if (!kvalid) dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     if (kvalid) {
       bf16* row = dqkv + ((int64_t)b * N + key) * ld_dqkv + h * 64;
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-        bf16x4 kv = {(bf16)(dk[dt][0] * scale), (bf16)(dk[dt][1] * scale), (bf16)(dk[dt][2] * scale),
-                     (bf16)(dk[dt][3] * scale)};
+        bf16x4 kv = {(bf16)dk[dt][0], (bf16)dk[dt][1], (bf16)dk[dt][2], (bf16)dk[dt][3]};
         bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
         *reinterpret_cast<bf16x4*>(row + D + dt * 16 + 4 * g) = kv;
         *reinterpret_cast<bf16x4*>(row + 2 * D + dt * 16 + 4 * g) = vv;
-        csk[dt] += dk[dt] * scale;
-        csv[dt] += dv[dt];
       }
     }
+    if (bias_part) {  // wave-uniform
+      cs[0] += colsum16(dk, lane);
+      cs[1] += colsum16(dv, lane);
+    }
   }
-  if (bias_part) bias_flush<2>(csk, &csv, smem, bias_part + (int64_t)b * 3 * D + h * 64, D);
+  if (bias_part) bias_flush_c<2>(cs, smem, bias_part + (int64_t)b * 3 * D + h * 64, D);
 }
 
 // ---------------------------------------------------------------------------
