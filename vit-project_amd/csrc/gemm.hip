@@ -886,17 +886,20 @@ using V4 = Cfg<256, 128, 32, 4, 2, 4, false, 4>;  //  96 KiB, 1 WG/CU, 4-deep ri
 //   P(i,r) = P[i*sPi + r*sPr], Q(j,r) = Q[j*sQj + r*sQr]
 // ----------------------------------------------------------------------------
 namespace gen {
-constexpr int TM = 64, TN = 64, TK = 16;
-template <typename T, int EPI, typename TO, typename TA>
+// TK 64: a quarter of the serial k-steps of 16.  TILE 64 (4x4 outputs per thread) or
+// 32 (2x2) -- the smaller tile when 64-tiles leave CUs idle (e.g. the 256-row head GEMMs).
+constexpr int TK = 64;
+template <int TILE, typename T, int EPI, typename TO, typename TA>
 __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ P, int64_t sPi, int64_t sPr,
                                                    const T* __restrict__ Q, int64_t sQj, int64_t sQr,
                                                    int M, int N, int R, int r_chunk, Epi e) {
+  constexpr int TM = TILE, TN = TILE, A = TILE / 16;
   __shared__ float Ps[TK][TM + 4];
   __shared__ float Qs[TK][TN + 4];
   const int tid = threadIdx.x, tx = tid & 15, ty = tid >> 4;
   const int i0 = blockIdx.y * TM, j0 = blockIdx.x * TN;
   const int rb = blockIdx.z * r_chunk, re = min(R, rb + r_chunk);
-  float acc[4][4] = {};
+  float acc[A][A] = {};
   for (int k0 = rb; k0 < re; k0 += TK) {
     for (int idx = tid; idx < TK * TM; idx += 256) {
       int kk = idx / TM, ii = idx % TM;
@@ -911,25 +914,25 @@ __global__ __launch_bounds__(256) void gemm_kernel(const T* __restrict__ P, int6
     __syncthreads();
 #pragma unroll
     for (int kk = 0; kk < TK; ++kk) {
-      float pv[4], qv[4];
+      float pv[A], qv[A];
 #pragma unroll
-      for (int a = 0; a < 4; ++a) pv[a] = Ps[kk][ty + 16 * a];
+      for (int a = 0; a < A; ++a) pv[a] = Ps[kk][ty + 16 * a];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) qv[b] = Qs[kk][tx * 4 + b];
+      for (int b = 0; b < A; ++b) qv[b] = Qs[kk][tx * A + b];
 #pragma unroll
-      for (int a = 0; a < 4; ++a)
+      for (int a = 0; a < A; ++a)
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc[a][b] = fmaf(pv[a], qv[b], acc[a][b]);
+        for (int b = 0; b < A; ++b) acc[a][b] = fmaf(pv[a], qv[b], acc[a][b]);
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int a = 0; a < 4; ++a) {
+  for (int a = 0; a < A; ++a) {
     int i = i0 + ty + 16 * a;
     if (i >= M) continue;
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      int j = j0 + tx * 4 + b;
+    for (int b = 0; b < A; ++b) {
+      int j = j0 + tx * A + b;
       if (j < N) epi1<EPI, TO, TA>(e, i, j, acc[a][b]);
     }
   }
@@ -1117,9 +1120,16 @@ static int launch_gen(const void* P, int64_t sPi, int64_t sPr, const void* Q, in
   if (r_chunk <= 0) r_chunk = gen::TK;
   int nz = (R + r_chunk - 1) / r_chunk;
   if (nz == 0) nz = 1;
-  dim3 grid((N + gen::TN - 1) / gen::TN, (M + gen::TM - 1) / gen::TM, nz);
-  hipLaunchKernelGGL((gen::gemm_kernel<T, EPI, TO, TA>), grid, dim3(256), 0, s,
-                     (const T*)P, sPi, sPr, (const T*)Q, sQj, sQr, M, N, R, r_chunk, e);
+  const int64_t big_tiles = (int64_t)((N + 63) / 64) * ((M + 63) / 64) * nz;
+  if (big_tiles < 256) {
+    dim3 grid((N + 31) / 32, (M + 31) / 32, nz);
+    hipLaunchKernelGGL((gen::gemm_kernel<32, T, EPI, TO, TA>), grid, dim3(256), 0, s,
+                       (const T*)P, sPi, sPr, (const T*)Q, sQj, sQr, M, N, R, r_chunk, e);
+  } else {
+    dim3 grid((N + 63) / 64, (M + 63) / 64, nz);
+    hipLaunchKernelGGL((gen::gemm_kernel<64, T, EPI, TO, TA>), grid, dim3(256), 0, s,
+                       (const T*)P, sPi, sPr, (const T*)Q, sQj, sQr, M, N, R, r_chunk, e);
+  }
   VIT_CHECK_LAUNCH();
   return 0;
 }

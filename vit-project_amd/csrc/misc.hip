@@ -2,6 +2,7 @@
 // GEMM operand), cls/pos fill and their grads, fused softmax-cross-entropy,
 // multi-tensor SGD (torch.optim.SGD semantics) with a bf16 shadow write, casts.
 #include "common.hpp"
+#include <type_traits>
 
 // ---------------------------------------------------------------------------
 // patch unfold: img f32 [B, C, Himg, Wimg] -> U [B*gh*gw, C*ps*ps] (T),
@@ -22,6 +23,21 @@ __global__ void patch_unfold_kernel(const float* __restrict__ img, T* __restrict
   const float* src = img + (((int64_t)b * C + c) * Hi + py * ps + ky) * Wi + px * ps;
   const int K = C * ps * ps;
   T* dst = U + ((int64_t)b * gh * gw + py * gw + px) * K + c * ps * ps + ky * ps;
+  if constexpr (std::is_same<T, bf16>::value) {
+    if (ps == 16 && (K % 8) == 0 && ((uintptr_t)U & 15) == 0 && (Wi % 4) == 0 && ((uintptr_t)img & 15) == 0) {
+      // one 64-B row segment in, two 16-B stores out (consecutive threads: consecutive patches)
+      f32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const f32x4*>(src + 4 * u);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 a = v[2 * h], b = v[2 * h + 1];
+        *reinterpret_cast<bf16x8*>(dst + 8 * h) =
+            bf16x8{(bf16)a[0], (bf16)a[1], (bf16)a[2], (bf16)a[3], (bf16)b[0], (bf16)b[1], (bf16)b[2], (bf16)b[3]};
+      }
+      return;
+    }
+  }
   if (ps % 4 == 0) {
     for (int kx = 0; kx < ps; kx += 4) {
       f32x4 v = *reinterpret_cast<const f32x4*>(src + kx);
@@ -42,6 +58,38 @@ __global__ void cls_pos_fill_kernel(float* __restrict__ x, const float* __restri
 }
 
 // dpos[t][j] = sum_b dx[b*S + t][j]; dcls[j] = dpos[0][j]
+// Vector path (S*D % 4 == 0): a workgroup owns 256 consecutive floats of the flattened
+// [S*D] (one f32x4 per lane); its POS_WAVES waves take interleaved images with four
+// independent accumulators each and combine through LDS in a fixed order (deterministic).
+constexpr int POS_WAVES = 8;
+__global__ __launch_bounds__(64 * POS_WAVES) void pos_grad_vec_kernel(const float* __restrict__ dx, int B, int64_t n,
+                                                                      float* __restrict__ dpos,
+                                                                      float* __restrict__ dcls, int D) {
+  __shared__ f32x4 red[POS_WAVES][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t c = ((int64_t)blockIdx.x * 64 + lane) * 4;
+  const bool ok = c < n;
+  f32x4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (ok) {
+    int b = wv;
+    for (; b + 3 * POS_WAVES < B; b += 4 * POS_WAVES) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc[u] += *reinterpret_cast<const f32x4*>(dx + (int64_t)(b + u * POS_WAVES) * n + c);
+    }
+    for (; b < B; b += POS_WAVES) acc[0] += *reinterpret_cast<const f32x4*>(dx + (int64_t)b * n + c);
+  }
+  red[wv][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (wv == 0 && ok) {
+    f32x4 s = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < POS_WAVES; ++w) s += red[w][lane];
+    *reinterpret_cast<f32x4*>(dpos + c) = s;
+    if (dcls && c < D) *reinterpret_cast<f32x4*>(dcls + c) = s;
+  }
+}
 __global__ void pos_grad_kernel(const float* __restrict__ dx, int B, int S, int D, float* __restrict__ dpos,
                                 float* __restrict__ dcls) {
   int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -180,6 +228,13 @@ int vit_cls_pos_fill(int B, int S, int D, float* x, const float* cls, const floa
 
 int vit_pos_grad(int B, int S, int D, const float* dx, float* dpos, float* dcls, void* stream) {
   int64_t n = (int64_t)S * D;
+  if (n % 4 == 0 && D % 4 == 0 && ((uintptr_t)dx & 15) == 0 && ((uintptr_t)dpos & 15) == 0 &&
+      ((uintptr_t)dcls & 15) == 0) {
+    hipLaunchKernelGGL(pos_grad_vec_kernel, dim3((unsigned)((n + 255) / 256)), dim3(64 * POS_WAVES), 0,
+                       (hipStream_t)stream, dx, B, n, dpos, dcls, D);
+    VIT_CHECK_LAUNCH();
+    return 0;
+  }
   hipLaunchKernelGGL(pos_grad_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, dx, B, S, D, dpos, dcls);
   VIT_CHECK_LAUNCH();
   return 0;
