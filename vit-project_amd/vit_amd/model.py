@@ -210,7 +210,7 @@ class _PatchEmbedFn(torch.autograd.Function):
                 ops.cast_bf16(rows.contiguous(), dxc)
         pw, pb, pc, pp = ctx.params
         dw = _gout(pw)
-        ops.linear_wgrad(dxc, U, out=dw.view(D, -1))
+        ops.linear_wgrad(dxc, U, out=dw.view(D, -1), tail=True)  # alone on the GPU after the join
         db = ops.colsum(dxc, out=_gout(pb))
         dpos, dcls = _gout(pp), _gout(pc)
         ops.pos_grad(dx, B, S, D, dpos, dcls)
@@ -329,13 +329,15 @@ class _BlockFn(torch.autograd.Function):
                                dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=g[7], dbeta=g[8],
                                dsum=g[6], reduce_on=side)
             # attention
+            # block 0 (the patch rows' block, last in the backward): its last weight gradients are the tail
+            tail = bool(compact_np)
             if ng[5]:
-                side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5]))
+                side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5], tail=tail))
             if need_attn:
                 do = ops.linear_dgrad(dxm_c, Wproj, out_dtype=T)
                 dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g[4], causal=causal)
                 if ng[3]:
-                    side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g[3]))
+                    side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g[3], tail=tail))
             if need_h1:
                 dh1 = ops.linear_dgrad(dqkv, Wqkv, out_dtype=T)
                 dx = torch.empty(M, D, dtype=torch.float32, device=dev)

@@ -115,25 +115,30 @@ def colreduce(part, S, N, out, accumulate=False, scratch=None):
 _WGRAD_WGS = [int(os.environ.get("VIT_WGRAD_WGS", "128"))]
 
 
-def _wgrad_split(M, N, K):
+# the backward's tail (block 0's last weight gradients, the patch embedding's): nothing else is
+# left to run beside them, so they split for the whole GPU
+_WGRAD_TAIL_WGS = [int(os.environ.get("VIT_WGRAD_TAIL_WGS", "256"))]
+
+
+def _wgrad_split(M, N, K, wgs=None):
     """Split of the M reduction so (256x256 output tiles) x split ~ _WGRAD_WGS workgroups
     (default 128: half the CUs, so the side-stream weight gradients leave CUs to the
     input-gradient chain on the main stream -- +1.3 % step rate vs 256): fp32 slab traffic split*N*K*8 bytes stays ~10% of the
     GEMM time."""
     tiles = max(1, ((N + 255) // 256) * ((K + 255) // 256))
-    want = max(1, round(_WGRAD_WGS[0] / tiles))
+    want = max(1, round((wgs or _WGRAD_WGS[0]) / tiles))
     return max(1, min(want, M // 1024))
 
 
-def linear_wgrad(dy2d, x2d, out=None, split=None):
-    """dW [N,K] (f32) = dy^T @ x,  dy [M,N], x [M,K]."""
+def linear_wgrad(dy2d, x2d, out=None, split=None, tail=False):
+    """dW [N,K] (f32) = dy^T @ x,  dy [M,N], x [M,K].  tail: split for _WGRAD_TAIL_WGS workgroups."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     assert x2d.shape[0] == M and x2d.dtype == dy2d.dtype
     if out is None:
         out = torch.empty(N, K, dtype=torch.float32, device=dy2d.device)
     if split is None:
-        split = _wgrad_split(M, N, K)
+        split = _wgrad_split(M, N, K, _WGRAD_TAIL_WGS[0] if tail else None)
     ws = workspace("wgrad", split * N * K * 4, dy2d.device) if split > 1 else None
     call("vit_linear_wgrad", L.dt(dy2d), M, N, K, ptr(dy2d), dy2d.stride(0), ptr(x2d), x2d.stride(0), ptr(out),
          split, ptr(ws), 0 if ws is None else ws.numel(), _s(dy2d))
