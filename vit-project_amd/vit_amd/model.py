@@ -72,6 +72,10 @@ _FWD_JOIN = [os.environ.get("VIT_FWD_JOIN", "end")]
 _BWD_JOIN = [os.environ.get("VIT_BWD_JOIN", "end")]
 # side-stream operands referenced until the next join (VIT_HOLD_REFS=0 only to demonstrate the race)
 _HOLD_REFS = [os.environ.get("VIT_HOLD_REFS", "1") != "0"]
+# images the caller's forward chain takes beyond B/2: at an even split the side chain ends
+# ~0.3 ms later (bs=256).  Default B/32 (8 at bs=256): +0.8 %; 16+ falls off a GEMM tile-count
+# cliff (-3 %).  profiles/r01/ab_fwd_half_split.json
+_FWD_HALF_DELTA = [None if os.environ.get("VIT_FWD_HALF_DELTA") is None else int(os.environ["VIT_FWD_HALF_DELTA"])]
 _HOLD = {}
 
 
@@ -264,7 +268,8 @@ class _BlockFn(torch.autograd.Function):
         if side.on and B >= 2 and T != torch.float32:
             # two half-batch chains on two streams: one chain's GEMM epilogues (HBM-bound)
             # overlap the other's MFMA main loops
-            hb = B // 2
+            delta = B // 32 if _FWD_HALF_DELTA[0] is None else _FWD_HALF_DELTA[0]
+            hb = min(B - 1, max(1, B // 2 + delta))
             side.run(lambda: chain(hb, B))
             side.guard(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act, xo)
             chain(0, hb)
