@@ -2,17 +2,27 @@
 
 One step = forward + mean cross-entropy + backward + fused SGD (lr 0.1, momentum
 0.9, wd 1e-4) on one synthetic batch already resident in HBM (VIT:132-147 minus
-the data loader).  N>1: one process per GPU (torchrun), 256 images per rank
-(weak scaling), gradients averaged with bucketed RCCL all-reduces (DDP in the
-reference, VIT:287).  Prints ONE JSON line on rank 0.
+the data loader).  N>1: one process per GPU, 256 images per rank (weak scaling),
+gradients averaged with RCCL all-reduces issued block by block during the
+backward (DDP in the reference, VIT:287).  Prints ONE JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-graph]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--graph]
+
+``--gpus N`` without a torchrun environment launches its own N ranks (one
+process per GPU, ``torch.distributed.run`` on 127.0.0.1, as the reference's
+``torchrun --nproc_per_node`` does: VSLURM:47) before anything touches the GPU.
+``--dry`` runs the same launcher and gradient-averaging path on CPU (gloo) with a
+stand-in gradient buffer: the multi-rank plumbing test (tests/test_bench_cli.py).
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
+import socket
+import statistics
+import subprocess
 import sys
 import time
 
@@ -20,20 +30,17 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "vit-project_amd"))
 
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
 FWD_FLOP_PER_IMG = 35.128e9          # SURVEY §8d (oracle.vit_flops_per_image)
 STEP_FLOP_PER_IMG = 3 * FWD_FLOP_PER_IMG
 # gfx950 dense bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk (16x16x32: 16384 FLOP / 16 clk) x 2.4 GHz
 PEAK_BF16_TFLOPS = 256 * 4 * 1024 * 2.4e9 / 1e12
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--graph", action="store_true",
                     help="replay one captured HIP graph per step (ROCm replays graph branches serially, so the "
@@ -41,13 +48,69 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="weight gradients inline instead of on a side stream")
-    return ap.parse_args()
+    ap.add_argument("--no-probe", action="store_true", help="no HIP events around the weight-gradient launches")
+    ap.add_argument("--dry", action="store_true", help="CPU/gloo launcher + gradient-averaging check, no GPU")
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------
+# rank launcher (before any GPU call)
+# ----------------------------------------------------------------------------
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int, argv) -> int:
+    """Start N ranks of this script under torch.distributed.run as child processes (never an
+    exec: the parent has not touched the GPU, and exits with the launcher's code)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+# ----------------------------------------------------------------------------
+# CPU baseline
+# ----------------------------------------------------------------------------
+
+def host_cpus():
+    """(threads usable by this process, os.cpu_count(), lscpu model name).  On the GPU box
+    os.cpu_count() reports the whole machine; the process's share is its affinity mask,
+    further capped by a cgroup CPU quota when one is set."""
+    total = os.cpu_count() or 1
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = total
+    for f in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            q, per = open(f).read().split()[:2]
+            if q != "max":
+                usable = min(usable, max(1, math.ceil(int(q) / int(per))))
+        except (OSError, ValueError):
+            pass
+    model = None
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return usable, total, model
 
 
 def cpu_baseline(seconds: float):
     """The oracle's fp32 ViT-B/16 train step (bs=4, configs[0]) on the host cores."""
+    import torch
     from oracle import vit_ref as R
-    threads = min(16, os.cpu_count() or 1)
+    threads, total, model = host_cpus()
     torch.set_num_threads(threads)
     cfg = R.VIT_B16
     p = R.init_params(cfg, seed=0)
@@ -65,29 +128,67 @@ def cpu_baseline(seconds: float):
         if el >= seconds or n >= 50:
             break
     return {"value": round(n * B / el, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "host_cpu_count": total, "cpu_model": model,
             "sample": f"{n} fp32 ViT-B/16 train steps (bs=4, fwd+CE+bwd+SGD) of oracle/vit_ref.py, "
-                      f"{el:.1f} s, torch CPU {threads} threads"}
+                      f"{el:.1f} s, torch CPU {threads} threads (the process's CPU share of {total})"}
 
 
-def _pmc_traffic():
-    """HBM bytes per launch of the roofline kernel from the committed counter passes
-    (tools/pmc_traffic.py; FETCH_SIZE doubled per the gfx950 correction), or None."""
-    f = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r01", "pmc_traffic_fc1_fwd_gelu.json")
-    try:
-        with open(f) as fh:
-            return int(json.load(fh)["traffic_bytes_per_launch"])
-    except (OSError, KeyError, ValueError):
-        return None
+def _pmc_traffic(name):
+    """HBM bytes per launch of a kernel from committed counter passes (tools/pmc_traffic.py;
+    FETCH_SIZE doubled per the gfx950 correction), or None."""
+    for rnd in ("r02", "r01"):
+        f = os.path.join(ROOT, "profiles", rnd, name)
+        try:
+            with open(f) as fh:
+                return int(json.load(fh)["traffic_bytes_per_launch"]), f"profiles/{rnd}/{name}"
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
 
 
-def main():
-    a = parse()
+# ----------------------------------------------------------------------------
+# dry run: launcher + gradient averaging on CPU (gloo)
+# ----------------------------------------------------------------------------
+
+def dry_main(a):
+    import torch
+    import torch.distributed as dist
+    from vit_amd import parallel
+    rank, world, _ = parallel.init_from_env("gloo")
+    n = 1 << 16
+    flat = torch.full((n,), float(rank + 1)) + torch.arange(n, dtype=torch.float32) * 1e-3
+    t0 = time.perf_counter()
+    for _ in range(max(1, a.steps)):
+        g = flat.clone()
+        parallel.allreduce_flat(g, bucket_mb=0.0625)
+    el = time.perf_counter() - t0
+    expect = torch.full((n,), (world + 1) / 2.0) + torch.arange(n, dtype=torch.float32) * 1e-3
+    ok = torch.allclose(g, expect, rtol=0, atol=1e-5)
+    oks = [None] * world if world > 1 else [ok]
+    if world > 1:
+        dist.all_gather_object(oks, ok)
+    if rank == 0:
+        print(json.dumps({"metric": "dry", "n_gpus": world, "ranks_ok": oks, "grad_avg_ok": all(oks),
+                          "steps": a.steps, "ms_per_step": round(el / max(1, a.steps) * 1e3, 3), "dry": True}),
+              flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if all(oks) else 1
+
+
+# ----------------------------------------------------------------------------
+# the benchmark
+# ----------------------------------------------------------------------------
+
+def main(a):
+    import torch
+    import torch.distributed as dist
     import vit_amd
     from vit_amd import parallel, ops
-    from vit_amd import _lib as L
 
     rank, world, local = parallel.init_from_env("nccl")
-    if world != a.gpus and "WORLD_SIZE" in os.environ:
+    if world != a.gpus:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE {world}", file=sys.stderr)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -96,6 +197,7 @@ def main():
     B = a.batch
     model = vit_amd.create_model("vit_base_patch16_224", num_classes=1000, compute_dtype=torch.bfloat16).to(dev)
     flat = model.use_flat_grads(True)
+    model.set_deferred_grad_join(True)  # gradients are read only after backward() returns
     vit_amd.set_wgrad_overlap(not a.no_overlap)
     opt = vit_amd.FusedSGD(model.parameters(), lr=0.1, momentum=0.9, weight_decay=1e-4)
     x = torch.randn(B, 3, 224, 224, device=dev)
@@ -106,91 +208,142 @@ def main():
     reducer = None
     if world > 1 and os.environ.get("VIT_DDP_OVERLAP", "1") != "0":
         reducer = parallel.OverlappedGradReduce(model)
+    main_stream = torch.cuda.Stream(device=dev)
+    red_events = []
 
-    def step():
+    def step(record=False):
         loss = vit_amd.cross_entropy(model(x), y)
         loss.backward()
-        if reducer is not None:
-            reducer.finish()
-        elif world > 1:
-            parallel.allreduce_flat(flat, bucket_mb=64.0)
+        if world > 1:
+            if record:
+                r0 = torch.cuda.Event(enable_timing=True)
+                r0.record()
+            if reducer is not None:
+                reducer.finish()
+            else:
+                parallel.allreduce_flat(flat, bucket_mb=64.0)
+            if record:
+                r1 = torch.cuda.Event(enable_timing=True)
+                r1.record()
+                red_events.append((r0, r1))
         opt.step()
         opt.zero_grad(set_to_none=True)
         return loss
 
     use_graph = a.graph and world == 1
-    s = torch.cuda.Stream(device=dev)
-    s.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(s):
+    with torch.cuda.stream(main_stream):
+        main_stream.wait_stream(torch.cuda.default_stream(dev))
         for _ in range(max(1, a.warmup)):
             loss = step()
-    torch.cuda.current_stream(dev).wait_stream(s)
-    torch.cuda.synchronize(dev)
-    warm_loss = float(loss.item())
-    del loss
-    graph = None
-    if use_graph:
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            gloss = step()
-        graph.replay()  # one untimed replay
         torch.cuda.synchronize(dev)
+        warm_loss = float(loss.item())
+        del loss
+        graph = None
+        if use_graph:
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                gloss = step()
+            graph.replay()  # one untimed replay
+            torch.cuda.synchronize(dev)
 
-    def run_steps(k):
-        for _ in range(k):
+        # --- timed region: exactly K steps, barrier + synchronize on both sides.  HIP events on
+        #     the caller's stream between steps give per-step times (median); HIP events around
+        #     every weight-gradient launch (on the side stream it runs on) give that kernel's
+        #     live in-step duration for the roofline line.
+        probe = [] if (not a.no_probe and graph is None) else None
+        ops.WGRAD_PROBE[0] = probe
+        marks = [torch.cuda.Event(enable_timing=True) for _ in range(a.steps + 1)]
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        marks[0].record()
+        for i in range(a.steps):
             if graph is not None:
                 graph.replay()
             else:
-                step()
-
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run_steps(a.steps)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
+                step(record=world > 1)
+            marks[i + 1].record()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        ops.WGRAD_PROBE[0] = None
+    step_ms = [marks[i].elapsed_time(marks[i + 1]) for i in range(a.steps)]
+    el_rank = el
+    per_rank = [el_rank]
     if world > 1:
         t = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, el_rank)
     final_loss = float(gloss.item()) if graph is not None else warm_loss
 
-    # --- dominant-kernel roofline: fc1 forward GEMM (M=B*197, N=3072, K=768, bias+GELU epilogue),
-    #     timed with HIP events on the stream it is launched on
-    blk = model.blocks[0]
+    # --- weight-gradient GEMMs (the step's dominant kernel class) in the timed steps
+    wg = None
+    if probe:
+        durs = [(e0.elapsed_time(e1), fl) for e0, e1, fl, mfma in probe if mfma]
+        per_step = len(durs) / a.steps
+        tot_ms = sum(d for d, _ in durs) / a.steps
+        tot_fl = sum(f for _, f in durs) / a.steps
+        wg = {"launches_per_step": per_step, "ms_per_step": round(tot_ms, 3),
+              "avg_launch_ms": round(tot_ms / per_step, 4), "flop_per_step": tot_fl,
+              "tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 1)}
+
+    # --- standalone leg of the same kernel: the fc1 weight gradient (dW1 = dpre^T h2, M = B*197,
+    #     N = 3072, K = 768) at the step's own split, alone on the GPU, HIP events on its stream
     M = B * 197
-    h = torch.randn(M, 768, device=dev).to(torch.bfloat16)
-    w1 = blk.mlp.fc1.weight._vit_shadow
-    b1 = blk.mlp.fc1.bias.detach()
-    pre = torch.empty(M, 3072, device=dev, dtype=torch.bfloat16)
-    act = torch.empty_like(pre)
-    # 20 warm-up launches: the first ones over the freshly allocated h / pre / act run ~20 % slower
-    # (tools/probe_fc1_data.py); the step reuses its buffers, so the steady state is what it sees
-    for _ in range(20):
-        ops.linear_fwd(h, w1, b1, epi=L.EPI_BIAS_GELU, out=pre, act_out=act)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    reps = 20
-    e0.record()
-    for _ in range(reps):
-        ops.linear_fwd(h, w1, b1, epi=L.EPI_BIAS_GELU, out=pre, act_out=act)
-    e1.record()
-    torch.cuda.synchronize(dev)
+    dpre = torch.randn(M, 3072, device=dev).to(torch.bfloat16)
+    h2 = torch.randn(M, 768, device=dev).to(torch.bfloat16)
+    dw = torch.empty(3072, 768, device=dev)
+    with torch.cuda.stream(main_stream):
+        for _ in range(20):
+            ops.linear_wgrad(dpre, h2, out=dw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 20
+        e0.record()
+        for _ in range(reps):
+            ops.linear_wgrad(dpre, h2, out=dw)
+        e1.record()
+        torch.cuda.synchronize(dev)
     k_ms = e0.elapsed_time(e1) / reps
     k_flop = 2.0 * M * 3072 * 768
     k_tflops = k_flop / (k_ms * 1e-3) / 1e12
+    red_ms = None
+    if red_events:
+        torch.cuda.synchronize(dev)
+        red_ms = statistics.median(r0.elapsed_time(r1) for r0, r1 in red_events)
 
     if rank != 0:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
-        return
+        return 0
     imgs = world * B * a.steps
     value = imgs / el
     ms = el / a.steps * 1e3
     step_tflops = value / world * STEP_FLOP_PER_IMG / 1e12
+    traffic, traffic_src = _pmc_traffic("pmc_traffic_wgrad_fc1.json")
+    if wg is not None:
+        roof = {"bound": "mfma", "kernel": "big::pp_kernel (split-K weight-gradient GEMM, 256x256x32 ping-pong) "
+                                           "+ its slab reduce: every bf16 dW = dY^T X of the step",
+                "achieved": wg["tflops"], "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
+                "frac": round(wg["tflops"] / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
+                "measured": "in-step: HIP events around each launch on the side stream it runs on, over the timed "
+                            "steps (its CUs are shared with the caller stream's kernels)",
+                "launches_per_step": wg["launches_per_step"], "ms_per_step": wg["ms_per_step"],
+                "avg_launch_ms": wg["avg_launch_ms"], "flop_per_step": wg["flop_per_step"],
+                "standalone": {"shape": "fc1 dW M=%d N=3072 K=768" % M, "ms": round(k_ms, 4),
+                               "achieved": round(k_tflops, 1), "frac": round(k_tflops / PEAK_BF16_TFLOPS, 4),
+                               "flop_per_launch": k_flop},
+                "traffic_unit": "HBM bytes per standalone fc1 launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc "
+                                "passes, %s)" % traffic_src}
+    else:
+        roof = {"bound": "mfma", "kernel": "big::pp_kernel fc1 weight gradient, standalone",
+                "achieved": round(k_tflops, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
+                "frac": round(k_tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "kernel_ms": round(k_ms, 4),
+                "flop_per_launch": k_flop}
     out = {
         "metric": "images/sec ViT-B/16 224 train step bs=256 (whole job)",
         "value": round(value, 2),
@@ -199,6 +352,7 @@ def main():
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms, 3),
+        "ms_per_step_median": round(statistics.median(step_ms), 3),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -208,23 +362,25 @@ def main():
                    "model": "vit_base_patch16_224", "global_batch": world * B, "per_gpu_batch": B,
                    "seq_len": 197, "parallelism": f"dp{world}", "launch": "hipgraph" if graph is not None else "eager",
                    "final_loss": round(final_loss, 4)},
-        "roofline": {"bound": "mfma", "kernel": "big::gemm_kernel<V5,RC,RC,BIAS_GELU> fc1 fwd, M=%d N=3072 K=768" % M,
-                     "achieved": round(k_tflops, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
-                     "frac": round(k_tflops / PEAK_BF16_TFLOPS, 4), "traffic": _pmc_traffic(),
-                     "traffic_unit": "bytes/launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc passes, "
-                                     "profiles/r01/pmc_traffic_fc1_fwd_gelu.json)",
-                     "algorithmic_bytes": (M * 768 + 3072 * 768 + 2 * M * 3072) * 2 + 3072 * 4,
-                     "kernel_ms": round(k_ms, 4), "flop_per_launch": k_flop},
+        "roofline": roof,
         "step_mfma": {"achieved_tflops": round(step_tflops, 1), "frac": round(step_tflops / PEAK_BF16_TFLOPS, 4),
                       "flop_per_img": STEP_FLOP_PER_IMG},
     }
+    if world > 1:
+        out["per_rank_s"] = [round(v, 4) for v in per_rank]
+        out["allreduce_exposed_ms_median"] = None if red_ms is None else round(red_ms, 3)
+        out["allreduce"] = "overlapped per block (side stream)" if reducer is not None else "bucketed after backward"
     if world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    sys.exit(dry_main(args) if args.dry else main(args))

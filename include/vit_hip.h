@@ -146,9 +146,14 @@ int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, 
 int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, const float* B, const float* gW,
                         const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
                         float* sdDnT_ws, void* unused, void* stream);
-/* torch.optim.AdamW step (NEWP:1181): tensors {p, g, exp_avg, exp_avg_sq, n}[]. */
-int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, const float* lr, const float* step,
-                   float beta1, float beta2, float eps, float weight_decay, void* stream);
+/* torch.optim.AdamW step (NEWP:1181, NEWP:1001): tensors {float* p; const float* g; float* exp_avg;
+ * float* exp_avg_sq; bf16* shadow (or null); int64 n; float step_size; float bc2_sqrt}[] where
+ * step_size = lr / (1 - beta1^step) and bc2_sqrt = sqrt(1 - beta2^step) for that tensor's own
+ * state['step'] (so a load_state_dict resume, NEWP:1189-1195, continues the bias correction);
+ * chunks as vit_sgd_step; decay = 1 - lr * weight_decay. */
+int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, float decay, float beta1, float beta2,
+                   float eps, void* stream);
+int vit_adamw_tensor_bytes(void);
 
 /* CLIP-HBA forward/loss around the towers (NEWP:287-304 -> clip_model(image, prompts, pos_embedding),
  * the CLIP-HBA fork, external; OpenAI-CLIP semantics assumed):

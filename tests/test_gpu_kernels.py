@@ -448,7 +448,76 @@ def test_fused_adamw_matches_torch():
         ref.step()
         opt.step()
     for p, q in zip(ps, qs):
-        _close(q, p, 1e-5, "adamw")
+        _close(q, p, 1e-6, "adamw")
+
+
+def test_fused_adamw_resume_continues_bias_correction():
+    """The sweep resume (NEWP:1189-1195: optimizer.load_state_dict of the saved state) must
+    continue each tensor's bias correction from its saved step, as torch.optim.AdamW does:
+    k steps, state_dict, a fresh optimizer loads it, more steps -- against torch doing the same."""
+    from vit_amd.optim import FusedAdamW
+    torch.manual_seed(2)
+    shapes = [(64, 96), (96,), (5,)]
+    ps = [torch.nn.Parameter(torch.randn(s)) for s in shapes]
+    qs = [torch.nn.Parameter(p.detach().clone().to(DEV)) for p in ps]
+    q_shadow = qs[0]
+    q_shadow._vit_shadow = torch.empty(q_shadow.shape, dtype=torch.bfloat16, device=DEV)
+    ref = torch.optim.AdamW(ps, lr=3e-4, weight_decay=0.01)
+    opt = FusedAdamW(qs, lr=3e-4, weight_decay=0.01)
+    grads = [[torch.randn(s) for s in shapes] for _ in range(9)]
+
+    def run(ref, opt, steps):
+        for gs in steps:
+            for p, q, g in zip(ps, qs, gs):
+                p.grad = g.clone()
+                q.grad = g.to(DEV)
+            ref.step()
+            opt.step()
+
+    run(ref, opt, grads[:5])
+    sd_ref, sd = ref.state_dict(), opt.state_dict()
+    assert [float(s["step"]) for s in sd["state"].values()] == [5.0] * 3
+    ref2 = torch.optim.AdamW(ps, lr=3e-4, weight_decay=0.01)
+    ref2.load_state_dict(sd_ref)
+    opt2 = FusedAdamW(qs, lr=3e-4, weight_decay=0.01)
+    # the state as a checkpoint holds it: CPU tensors (torch.save -> torch.load map_location cpu)
+    sd_cpu = {"state": {k: {n: t.cpu() for n, t in v.items()} for k, v in sd["state"].items()},
+              "param_groups": sd["param_groups"]}
+    opt2.load_state_dict(sd_cpu)
+    run(ref2, opt2, grads[5:])
+    for p, q in zip(ps, qs):
+        _close(q, p, 1e-6, "adamw resumed")
+    assert all(float(opt2.state[q]["step"]) == 9.0 for q in qs)
+    # the bf16 GEMM shadow was rewritten in the same pass and is marked fresh
+    assert torch.equal(q_shadow._vit_shadow.cpu(), q_shadow.detach().cpu().to(torch.bfloat16))
+    assert q_shadow._vit_shadow_version == q_shadow._version
+
+
+def test_fused_adamw_update_reaches_bf16_forward():
+    """A ViT in bf16 trained by FusedAdamW: the next forward must use the updated weights
+    (the shadow the GEMMs read is refreshed), i.e. equal a fresh model loaded with them."""
+    import vit_amd
+    from oracle import vit_ref as R
+    cfg = R.ViTConfig(img_size=32, patch_size=16, embed_dim=128, depth=2, num_heads=2, num_classes=10)
+    p = R.init_params(cfg, seed=4, random_affine=True)
+    kw = dict(img_size=32, patch_size=16, embed_dim=128, depth=2, num_heads=2, num_classes=10,
+              compute_dtype=torch.bfloat16)
+    m = vit_amd.VisionTransformer(**kw)
+    m.load_state_dict(p)
+    m = m.to(DEV)
+    x = torch.randn(4, 3, 32, 32, generator=torch.Generator().manual_seed(5)).to(DEV)
+    y = torch.tensor([1, 2, 3, 4], device=DEV)
+    opt = vit_amd.FusedAdamW(m.parameters(), lr=1e-2)
+    vit_amd.cross_entropy(m(x), y).backward()
+    opt.step()
+    with torch.no_grad():
+        after = m(x)
+    m2 = vit_amd.VisionTransformer(**kw)
+    m2.load_state_dict({k: v.cpu() for k, v in m.state_dict().items()})
+    m2 = m2.to(DEV)
+    with torch.no_grad():
+        fresh = m2(x)
+    assert torch.equal(after, fresh)
 
 
 def test_dora_weight_matches_reference_fixture(golden_dir):

@@ -88,29 +88,33 @@ __global__ __launch_bounds__(256) void dora_bwd_row_kernel(int in, int out, cons
 }
 
 // ---------------------------------------------------------------------------
-// AdamW (torch.optim.AdamW, amsgrad off): decoupled decay then Adam update.
+// AdamW (torch.optim.AdamW, amsgrad off, single-tensor path): decoupled decay,
+// lerp'd first moment, then p -= step_size * m / (sqrt(v)/sqrt(bc2) + eps).
+// step_size = lr / (1 - b1^step) and sqrt(1 - b2^step) are computed per tensor in
+// double on the host from that tensor's own state['step'] (as torch does), so a
+// resumed optimizer (load_state_dict) continues the bias correction where it was.
+// The bf16 GEMM shadow of the parameter (if any) is written in the same pass.
 // ---------------------------------------------------------------------------
-struct AdamTensor { float* p; const float* g; float* m; float* v; int64_t n; };
+struct AdamTensor { float* p; const float* g; float* m; float* v; bf16* shadow; int64_t n; float step_size; float bc2_sqrt; };
 struct AdamChunk { int tensor; int pad; int64_t start; };
 constexpr int ADAM_CHUNK = 4096;
 
 __global__ __launch_bounds__(256) void adamw_kernel(const AdamTensor* __restrict__ ts, const AdamChunk* __restrict__ chunks,
-                                                    const float* __restrict__ lr_ptr, const float* __restrict__ step_ptr,
-                                                    float b1, float b2, float eps, float wd) {
+                                                    float decay, float b1, float b2, float eps) {
   const AdamChunk ch = chunks[blockIdx.x];
   const AdamTensor t = ts[ch.tensor];
-  const float lr = *lr_ptr, step = *step_ptr;
-  const float bc1 = 1.f - powf(b1, step), bc2 = 1.f - powf(b2, step);
-  const float step_size = lr / bc1, bc2s = sqrtf(bc2);
+  const float w1 = 1.f - b1, w2 = 1.f - b2;
   const int64_t end = min(t.n, ch.start + ADAM_CHUNK);
   for (int64_t i = ch.start + threadIdx.x; i < end; i += 256) {
-    float p = t.p[i] * (1.f - lr * wd);
-    float g = t.g[i];
-    float m = t.m[i] * b1 + (1.f - b1) * g;      // lerp(m, g, 1-b1)
-    float v = t.v[i] * b2 + (1.f - b2) * g * g;
-    float denom = sqrtf(v) / bc2s + eps;
-    p -= step_size * m / denom;
+    float p = __fmul_rn(t.p[i], decay);
+    const float g = t.g[i];
+    float m = t.m[i];
+    m = __fadd_rn(m, __fmul_rn(w1, __fsub_rn(g, m)));  // torch lerp, weight < 0.5 branch
+    float v = __fadd_rn(__fmul_rn(t.v[i], b2), __fmul_rn(__fmul_rn(w2, g), g));
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), t.bc2_sqrt), eps);
+    p = __fsub_rn(p, __fmul_rn(t.step_size, __fdiv_rn(m, denom)));
     t.p[i] = p; t.m[i] = m; t.v[i] = v;
+    if (t.shadow) t.shadow[i] = (bf16)p;
   }
 }
 
@@ -150,15 +154,16 @@ int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, 
                   stream);
 }
 
-// Fused AdamW over a table of AdamTensor {p, g, m, v, n}; chunks of 4096 elements
-// {tensor, pad, start}; lr and step (1-based, float) are device scalars.
-int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, const float* lr, const float* step, float beta1,
-                   float beta2, float eps, float weight_decay, void* stream) {
+// Fused AdamW over a table of AdamTensor {p, g, m, v, shadow, n, step_size, bc2_sqrt};
+// chunks of 4096 elements {tensor, pad, start}; decay = 1 - lr * weight_decay.
+int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, float decay, float beta1, float beta2,
+                   float eps, void* stream) {
   if (nchunks <= 0) return 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, (const AdamTensor*)tensors,
-                     (const AdamChunk*)chunks, lr, step, beta1, beta2, eps, weight_decay);
+                     (const AdamChunk*)chunks, decay, beta1, beta2, eps);
   VIT_CHECK_LAUNCH();
   return 0;
 }
+int vit_adamw_tensor_bytes(void) { return (int)sizeof(AdamTensor); }
 
 }  // extern "C"

@@ -140,9 +140,22 @@ def linear_wgrad(dy2d, x2d, out=None, split=None, tail=False):
     if split is None:
         split = _wgrad_split(M, N, K, _WGRAD_TAIL_WGS[0] if tail else None)
     ws = workspace("wgrad", split * N * K * 4, dy2d.device) if split > 1 else None
+    probe = WGRAD_PROBE[0]
+    if probe is not None:  # bench.py: HIP events around this launch, on the stream it runs on
+        e0 = torch.cuda.Event(enable_timing=True)
+        e0.record()
     call("vit_linear_wgrad", L.dt(dy2d), M, N, K, ptr(dy2d), dy2d.stride(0), ptr(x2d), x2d.stride(0), ptr(out),
          split, ptr(ws), 0 if ws is None else ws.numel(), _s(dy2d))
+    if probe is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        probe.append((e0, e1, 2.0 * M * N * K, L.dt(dy2d) == L.BF16 and M % 32 == 0))
     return out
+
+
+# bench.py's live roofline of the weight-gradient GEMMs: a list to collect
+# (start event, end event, flop, on the MFMA path) per vit_linear_wgrad launch, or None
+WGRAD_PROBE = [None]
 
 
 def colsum(x2d, out=None, accumulate=False):

@@ -35,8 +35,9 @@ def _table(entries, struct_fields):
 class _MultiTensor:
     CHUNK = 4096
 
-    def __init__(self, device):
+    def __init__(self, device, fields=5):
         self.device = device
+        self.fields = fields
         self._key = None
         self._tdev = None
         self._cdev = None
@@ -51,7 +52,7 @@ class _MultiTensor:
             raise RuntimeError("optimizer tensor table changed during HIP-graph capture: enable "
                                "model.use_flat_grads() so gradient addresses are fixed, and warm up once "
                                "before capturing")
-        t = _table(entries, 5)
+        t = _table(entries, self.fields)
         chunks = []
         for i, n in enumerate(sizes):
             for s in range(0, n, self.CHUNK):
@@ -138,21 +139,41 @@ class FusedSGD(torch.optim.Optimizer):
         self._mt.build(entries, sizes)
         call("vit_sgd_step", self._mt._tdev.data_ptr(), self._mt._cdev.data_ptr(), self._mt.nchunks,
              self._lr_dev.data_ptr(), float(mom), float(wd), L.stream_ptr(dev))
-        # shadows are now in sync with the (raw-pointer) update; mark them fresh
+        # raw-pointer update: bump versions; the shadows the kernel wrote stay fresh
         for g in self.param_groups:
             for p in g["params"]:
-                if getattr(p, "_vit_shadow", None) is not None and p.grad is not None:
-                    p._vit_shadow_version = p._version
+                if p.grad is not None:
+                    _mark_updated(p)
         return loss
 
 
+def _f32_pair(a: float, b: float) -> int:
+    """Two float32 values packed little-endian into one int64 table slot."""
+    return int(np.array([a, b], dtype=np.float32).view(np.int64)[0])
+
+
+def _mark_updated(p: torch.Tensor):
+    """A parameter was rewritten through a raw pointer: bump its version counter (what an
+    in-place torch op would do), so version-keyed caches (the bf16 GEMM shadow, the CLIP
+    frozen-prefix cache) see the change; a shadow the kernel itself rewrote stays fresh."""
+    torch.autograd.graph.increment_version(p)
+    if getattr(p, "_vit_shadow", None) is not None:
+        p._vit_shadow_version = p._version
+
+
 class FusedAdamW(torch.optim.Optimizer):
+    """torch.optim.AdamW (NEWP:1181; amsgrad off, maximize off) as one launch per group.
+
+    Per-parameter state matches torch's (``step`` a float32 scalar tensor, ``exp_avg``,
+    ``exp_avg_sq``), so ``state_dict()`` / ``load_state_dict()`` round-trip with
+    ``torch.optim.AdamW`` and a resumed optimizer (NEWP:1189-1195) continues each tensor's
+    bias correction from its saved ``step``.  Bias corrections are computed in double on the
+    host per tensor, as torch's single-tensor path does; the kernel also refreshes the bf16
+    GEMM shadow of shadowed weights."""
+
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
-        self._mt = None
-        self._lr_dev = None
-        self._step_dev = None
-        self._nstep = 0
+        self._mt = {}
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -160,38 +181,41 @@ class FusedAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
-        g0 = self.param_groups[0]
-        dev = g0["params"][0].device
-        L.require_gpu(torch.empty(0, device=dev))
-        if self._mt is None:
-            self._mt = _MultiTensor(dev)
-            self._lr_dev = torch.empty(1, dtype=torch.float32, device=dev)
-            self._step_dev = torch.empty(1, dtype=torch.float32, device=dev)
-        self._nstep += 1
-        self._lr_dev.fill_(float(g0["lr"]))
-        self._step_dev.fill_(float(self._nstep))
-        entries, sizes = [], []
-        for p in g0["params"]:
-            if p.grad is None:
+        for gi, group in enumerate(self.param_groups):
+            params = [p for p in group["params"] if p.grad is not None]
+            if not params:
                 continue
-            st = self.state[p]
-            if "exp_avg" not in st:
-                st["exp_avg"] = torch.zeros_like(p)
-                st["exp_avg_sq"] = torch.zeros_like(p)
-                st["step"] = torch.zeros((), dtype=torch.float32)
-            st["step"] += 1
-            if not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
-                p.grad = p.grad.float().contiguous()
-            entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(),
-                            st["exp_avg_sq"].data_ptr(), p.numel()))
-            sizes.append(p.numel())
-        if not entries:
-            return loss
-        self._mt.build(entries, sizes)
-        b1, b2 = g0["betas"]
-        call("vit_adamw_step", self._mt._tdev.data_ptr(), self._mt._cdev.data_ptr(), self._mt.nchunks,
-             self._lr_dev.data_ptr(), self._step_dev.data_ptr(), float(b1), float(b2), float(g0["eps"]),
-             float(g0["weight_decay"]), L.stream_ptr(dev))
+            dev = params[0].device
+            L.require_gpu(torch.empty(0, device=dev))
+            lr, (b1, b2), eps, wd = float(group["lr"]), group["betas"], float(group["eps"]), float(group["weight_decay"])
+            entries, sizes = [], []
+            for p in params:
+                st = self.state[p]
+                if len(st) == 0:
+                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["step"] += 1
+                step = float(st["step"].item())
+                bc1 = 1.0 - b1 ** step
+                bc2 = 1.0 - b2 ** step
+                if not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
+                    p.grad = p.grad.float().contiguous()
+                for k in ("exp_avg", "exp_avg_sq"):
+                    if st[k].device != p.device or not st[k].is_contiguous():
+                        st[k] = st[k].to(p.device).contiguous()
+                sh = getattr(p, "_vit_shadow", None)
+                entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                                None if sh is None else sh.data_ptr(), p.numel(), _f32_pair(lr / bc1, math.sqrt(bc2))))
+                sizes.append(p.numel())
+            mt = self._mt.get(gi)
+            if mt is None:
+                mt = self._mt[gi] = _MultiTensor(dev, fields=7)
+            mt.build(entries, sizes)
+            call("vit_adamw_step", mt._tdev.data_ptr(), mt._cdev.data_ptr(), mt.nchunks, float(1.0 - lr * wd),
+                 float(b1), float(b2), eps, L.stream_ptr(dev))
+            for p in params:
+                _mark_updated(p)
         return loss
 
 

@@ -79,6 +79,8 @@ class OverlappedGradReduce:
         self.use_avg = dist.get_backend(group) == "nccl"  # gloo has no AVG: SUM, then divide
         self.pending, self.covered = [], []
         model.set_grad_ready_hook(self._span_ready)
+        if hasattr(model, "set_deferred_grad_join"):
+            model.set_deferred_grad_join(True)  # gradients are read only in finish()
 
     def _reduce(self, lo, hi):
         seg = self.flat[lo:hi]
