@@ -13,7 +13,9 @@ VIT_FWD_HALF_DELTA = B/32: M = 26 792 / 23 640 token rows, ragged GEMM tiles).
       batch (the fp32 path is pinned to the golden fixtures at 1e-3 in test_gpu_parity.py):
       per-tensor cosine >= 0.999 and norm within 2 %;
   (c) a 30-step bs=32 SGD loss trajectory (lr 0.02 = the reference's warm-up epoch-1 LR,
-      momentum 0.9, wd 1e-4) in bf16 against the fp32 HIP path: every step within 1 %.
+      momentum 0.9, wd 1e-4) in bf16 against the fp32 HIP path: every step within 1 % (a
+      0.01-nat floor once the memorised batch's loss nears 0), and the 30-step parameter change
+      of every tensor with cosine >= 0.99 between the two.
 """
 import pytest
 import torch
@@ -109,7 +111,7 @@ def test_bf16_loss_trajectory_tracks_f32_30_steps():
     g = torch.Generator().manual_seed(20)
     x = torch.randn(32, 3, 224, 224, generator=g).to(DEV)
     y = torch.randint(0, 1000, (32,), generator=g).to(DEV)
-    traj = {}
+    traj, delta = {}, {}
     for dt in (torch.bfloat16, torch.float32):
         m = _bench_model(p, dt)
         opt = vit_amd.FusedSGD(m.parameters(), lr=0.02, momentum=0.9, weight_decay=1e-4)
@@ -121,7 +123,14 @@ def test_bf16_loss_trajectory_tracks_f32_30_steps():
             opt.zero_grad(set_to_none=True)
             ls.append(float(loss.item()))
         traj[dt] = ls
+        delta[dt] = {k: (v.float().cpu() - p[k]) for k, v in m.state_dict().items()}
     a, b = traj[torch.bfloat16], traj[torch.float32]
-    assert b[-1] < b[0]  # the run does train
-    rel = [abs(u - v) / abs(v) for u, v in zip(a, b)]
-    assert max(rel) <= 0.01, list(zip(a, b))
+    assert b[-1] < 0.1 * b[0]  # the batch is memorised within the 30 steps (7.19 -> ~0.5 by step 6)
+    # 1 % relative, with a 0.01-nat floor once the loss has collapsed toward 0
+    err = [abs(u - v) / max(abs(v), 1.0) for u, v in zip(a, b)]
+    assert max(err) <= 0.01, list(zip(a, b))
+    # drift: what 30 steps changed in every parameter tensor points the same way in both
+    for k in delta[torch.float32]:
+        u, v = delta[torch.bfloat16][k].flatten().double(), delta[torch.float32][k].flatten().double()
+        cos = torch.nn.functional.cosine_similarity(u, v, dim=0).item()
+        assert cos >= 0.99, (k, cos)

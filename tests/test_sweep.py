@@ -150,11 +150,99 @@ def test_run_sweep_shards_and_resumes_from_baseline(tmp_path):
         done += S.run_sweep(_make, crit, data, conds, rank=rank, world=2, perturb_type="label_shuffle",
                             out_dir=str(tmp_path / "sweep"), baseline_dora_path=str(base / "dora"),
                             baseline_random_state_path=str(base / "rs"), epochs=4, batch_size=32)
-    assert sorted(c for c, _ in done) == sorted(conds)  # every condition exactly once over the ranks
-    for (start, length), res in done:
+    assert sorted(c for c, _, _ in done) == sorted(conds)  # every condition exactly once over the ranks
+    for (start, length), res, _ in done:
         with open(res) as fh:
             rows = list(csv.reader(fh))[1:]
         # resumed at epoch start-1: rows for epochs start..4, shuffles flagged inside the window only
         assert [int(r[0]) for r in rows] == list(range(start, 5))
         flags = [r[6] == "True" for r in rows]
         assert flags == [P.in_window(int(r[0]) - 1, start, length) for r in rows]
+
+
+def test_reference_grid_is_the_136_conditions_on_disk():
+    grid = S.reference_length_grid()
+    assert len(grid) == 136 and len(set(grid)) == 136
+    starts = sorted({e for e, _ in grid})
+    assert starts == [1, 2, 3, 6, 7, 8, 10, 13, 16, 19, 20, 22, 30, 40, 50, 58, 60, 70, 80, 90, 94]
+    assert {l for _, l in grid} == {2, 5, 10, 20, 30, 40, 50}
+    assert (22, 5) in grid and (22, 2) not in grid and (13, 2) not in grid and (94, 50) in grid
+    from vit_amd import parallel
+    assert parallel.length_sweep_conditions() == grid
+    ref = "/root/reference/Data/clip_results/perturb_length_experiments_baselineseed1_perturbseed0"
+    if os.path.isdir(ref):  # build container only: the directory names themselves
+        names = sorted(os.listdir(ref))
+        assert sorted(os.path.basename(S.condition_dir("", "random_target", e, l)) for e, l in grid) == names
+    # 8-way shards: every condition exactly once, start-epoch chains never split
+    seen = []
+    for r in range(8):
+        mine = parallel.shard_conditions(grid, 8, r)
+        seen += mine
+        for e in {e for e, _ in mine}:
+            assert sorted(c for c in mine if c[0] == e) == sorted(c for c in grid if c[0] == e)
+    assert sorted(seen) == grid
+
+
+def _baseline(tmp_path, data, epochs):
+    m, opt = _make()
+    base = tmp_path / "baseline"
+    S.train_condition(m, opt, nn.MSELoss(), data, epochs=epochs, training_run=1, perturb_length=0, perturb_type=None,
+                      batch_size=32, training_res_path=str(tmp_path / "base.csv"),
+                      dora_parameters_path=str(base / "dora"), random_state_path=str(base / "rs"),
+                      dataloader_generator=torch.Generator().manual_seed(0))
+    return str(base / "dora"), str(base / "rs")
+
+
+def _rows(path):
+    with open(path) as fh:
+        return list(csv.reader(fh))
+
+
+def test_sibling_resume_is_exact(tmp_path):
+    """LEN:188-256: a longer window resumes from the longest shorter sibling at epoch
+    start-1+sibling_length -- and gives exactly the rows a run from the baseline gives."""
+    data = _data(2)
+    bd, br = _baseline(tmp_path, data, 4)
+    kw = dict(perturb_type="random_target", baseline_dora_path=bd, baseline_random_state_path=br, epochs=9,
+              batch_size=32, early_stopping_patience=50)
+    chained = S.run_sweep(_make, nn.MSELoss(), data, [(3, 2), (3, 5)], out_dir=str(tmp_path / "a"), **kw)
+    assert [src for _, _, src in chained] == ["baseline", "sibling l2"]
+    alone = S.run_sweep(_make, nn.MSELoss(), data, [(3, 5)], out_dir=str(tmp_path / "b"), **kw)
+    assert alone[0][2] == "baseline"
+    got, ref = _rows(chained[1][1]), _rows(alone[0][1])
+    assert got[0] == S.CSV_HEADERS and [int(r[0]) for r in got[1:]] == list(range(3, 10))
+    assert got == ref  # bit-identical losses / rho: the resume restored model, optimizer, RNG and loader state
+    sib = _rows(chained[0][1])
+    assert got[1:3] == sib[1:3]  # epochs 3..4 (through the sibling's window end) copied from the sibling
+    # own-CSV resume: a finished condition is skipped, a truncated one continues in place
+    again = S.run_sweep(_make, nn.MSELoss(), data, [(3, 5)], out_dir=str(tmp_path / "a"), **kw)
+    assert again[0][2] == "complete"
+
+
+def test_launch_sweep_world8_covers_every_condition_once(tmp_path):
+    """The 8-process launcher (one process per GPU on the box; CPU workers here) over a
+    scaled-down grid with the reference grid's structure: chains per start epoch stay on one
+    rank, every condition runs exactly once, longer windows resume from their siblings."""
+    data = _data(3, n_train=64, n_test=16)
+    bd, br = _baseline(tmp_path, data, 15)
+    starts = [1, 2, 3, 6, 7, 8, 10, 13, 16]
+    conds = [(e, l) for e in starts for l in (2, 5)]
+    res = S.launch_sweep(8, _make, nn.MSELoss(), data, conds, perturb_type="random_target",
+                         out_dir=str(tmp_path / "sw"), baseline_dora_path=bd, baseline_random_state_path=br,
+                         epochs=20, batch_size=32, early_stopping_patience=50, torch_threads=1)
+    assert sorted(res) == list(range(8))
+    flat = [c for r in res.values() for c, _, _ in r]
+    assert sorted(flat) == sorted(conds)
+    src = {c: s for r in res.values() for c, _, s in r}
+    assert all(src[(e, 2)] == "baseline" and src[(e, 5)] == "sibling l2" for e in starts)
+    for r, items in res.items():
+        assert {c for c, _, _ in items} == set(parallel_shard(conds, r))
+    for (e, l), path, _ in (x for r in res.values() for x in r):
+        rows = _rows(path)
+        assert [int(v[0]) for v in rows[1:]] == list(range(e, 21))
+        assert [v[5] == "True" for v in rows[1:]] == [P.in_window(int(v[0]) - 1, e, l) for v in rows[1:]]
+
+
+def parallel_shard(conds, r):
+    from vit_amd import parallel
+    return parallel.shard_conditions(conds, 8, r)

@@ -130,7 +130,12 @@ def shard_conditions(conditions: Sequence[Tuple[int, int]], world: int, rank: in
     return sorted(mine, key=lambda c: (c[0], c[1]))
 
 
-def length_sweep_conditions(max_epoch: int = 16, lengths: Iterable[int] = (1, 2, 4, 8, 16, 32, 64, 100)):
-    """A start x duration grid in the shape of the reference's 136-condition sweep
-    (README:47-48); the exact grid is a driver argument (LEN:42-83)."""
-    return [(e, l) for e in range(1, max_epoch + 1) for l in lengths if l <= 100]
+def length_sweep_conditions(starts=None, lengths=None):
+    """The start x duration conditions of the length sweep (LEN:42-83).  Default: the reference's
+    own 136-condition grid (``sweep.reference_length_grid``, README:47-48); with ``starts`` /
+    ``lengths`` the full product of the two."""
+    if starts is None and lengths is None:
+        from .sweep import reference_length_grid
+        return reference_length_grid()
+    from .sweep import REFERENCE_LENGTHS
+    return [(e, l) for e in (starts or range(1, 17)) for l in (lengths or REFERENCE_LENGTHS)]

@@ -154,18 +154,35 @@ def behavioral_rsa(model, inference_images, reference_rdm, batch_size=16):
 def train_condition(model, optimizer, criterion, data, *, epochs, training_run, perturb_length, perturb_type,
                     perturb_seed=42, perturb_distribution="target", batch_size=64, early_stopping_patience=5,
                     training_res_path, dora_parameters_path, random_state_path, dataloader_generator,
-                    resume_from_epoch=0, modules=DORA_MODULES):
+                    resume_from_epoch=0, previous_training_res_path=None, modules=DORA_MODULES):
     """The epoch loop of NEWP:train_model for one (training_run, perturb_length) condition.
 
     ``data`` = dict(train=(images, targets), test=(images, targets), inference=images,
     reference_rdm=ndarray[48, 48]).  Target mean / std for the perturbations are the scalar
-    mean / std over all training targets (NEWP:1098-1105, quirk Q4)."""
+    mean / std over all training targets (NEWP:1098-1105, quirk Q4).
+
+    CSV start (NEWP:797-834): resuming in place (``previous_training_res_path`` is this CSV)
+    appends; otherwise the file is rewritten with the header and, when resuming from another
+    run (a shorter sibling, LEN:246-253), that run's rows for epochs <= ``resume_from_epoch``."""
     tr_x, tr_y = data["train"]
     te_x, te_y = data["test"]
     mean, std = float(tr_y.mean()), float(tr_y.std())
-    if resume_from_epoch == 0 or not os.path.exists(training_res_path):
+    in_place = (previous_training_res_path == training_res_path and os.path.exists(training_res_path)
+                and resume_from_epoch > 0)
+    if not in_place:
         with open(training_res_path, "w", newline="") as fh:
-            csv.writer(fh).writerow(CSV_HEADERS)
+            w = csv.writer(fh)
+            w.writerow(CSV_HEADERS)
+            if previous_training_res_path and resume_from_epoch > 0 and os.path.exists(previous_training_res_path):
+                with open(previous_training_res_path, newline="") as prev:
+                    r = csv.reader(prev)
+                    next(r, None)
+                    for row in r:
+                        try:
+                            if int(row[0]) <= resume_from_epoch:
+                                w.writerow(row)
+                        except (ValueError, IndexError):
+                            continue
     stopper = P.EarlyStopping(early_stopping_patience, training_run, perturb_length)
     rows = []
     model.train()
@@ -199,29 +216,173 @@ def train_condition(model, optimizer, criterion, data, *, epochs, training_run, 
     return rows
 
 
+# The 136 (start epoch, length) conditions of the reference's length sweep, as they are on disk
+# under Data/clip_results/perturb_length_experiments_baselineseed1_perturbseed0/random_target_e{E}_l{L}
+# (README:47-48): 21 start epochs x lengths {2, 5, 10, 20, 30, 40, 50}, less the 11 that were
+# not run (length 2 at starts 13, 16, 19, 58, 94; start 22 only at length 5).
+REFERENCE_LENGTHS = (2, 5, 10, 20, 30, 40, 50)
+_REFERENCE_STARTS = {1: REFERENCE_LENGTHS, 2: REFERENCE_LENGTHS, 3: REFERENCE_LENGTHS, 6: REFERENCE_LENGTHS,
+                     7: REFERENCE_LENGTHS, 8: REFERENCE_LENGTHS, 10: REFERENCE_LENGTHS, 13: REFERENCE_LENGTHS[1:],
+                     16: REFERENCE_LENGTHS[1:], 19: REFERENCE_LENGTHS[1:], 20: REFERENCE_LENGTHS, 22: (5,),
+                     30: REFERENCE_LENGTHS, 40: REFERENCE_LENGTHS, 50: REFERENCE_LENGTHS,
+                     58: REFERENCE_LENGTHS[1:], 60: REFERENCE_LENGTHS, 70: REFERENCE_LENGTHS,
+                     80: REFERENCE_LENGTHS, 90: REFERENCE_LENGTHS, 94: REFERENCE_LENGTHS[1:]}
+
+
+def reference_length_grid() -> List[Tuple[int, int]]:
+    """The reference's 136-condition start x duration grid (sorted by start, then length)."""
+    return [(e, l) for e in sorted(_REFERENCE_STARTS) for l in _REFERENCE_STARTS[e]]
+
+
+def condition_dir(out_dir, perturb_type, start, length):
+    """LEN's per-condition output directory name (``--output_dir random_target_e2_l2``)."""
+    return os.path.join(out_dir, f"{perturb_type}_e{start}_l{length}")
+
+
+def last_completed_epoch(csv_path) -> int:
+    """LEN:137-160: the largest (1-based) epoch in an existing results CSV, 0 if none."""
+    last = 0
+    if not os.path.exists(csv_path):
+        return 0
+    with open(csv_path, newline="") as fh:
+        r = csv.reader(fh)
+        next(r, None)
+        for row in r:
+            try:
+                last = max(last, int(row[0]))
+            except (ValueError, IndexError):
+                continue
+    return last
+
+
+def find_previous_run_dir(base_dir, perturb_type, start_epoch, current_length):
+    """LEN:188-218: the run directory with the same start epoch (token ``e{start}_``, and the
+    perturbation type as the name prefix) and the longest length below ``current_length``;
+    returns (dir, length) or (None, None).  Candidates longest first (see ``resume_plan``)."""
+    c = _sibling_candidates(base_dir, perturb_type, start_epoch, current_length)
+    return c[0] if c else (None, None)
+
+
+def _sibling_candidates(base_dir, perturb_type, start_epoch, current_length):
+    out = []
+    if not os.path.isdir(base_dir):
+        return out
+    for name in os.listdir(base_dir):
+        full = os.path.join(base_dir, name)
+        if not os.path.isdir(full) or f"e{start_epoch}_" not in name:
+            continue
+        if perturb_type in ("random_target", "label_shuffle") and not name.startswith(perturb_type):
+            continue
+        length = next((int(p[1:]) for p in name.split("_") if p.startswith("l") and p[1:].isdigit()), None)
+        if length is not None and length < current_length:
+            out.append((full, length))
+    return sorted(out, key=lambda t: -t[1])
+
+
+def resume_plan(out_dir, perturb_type, start, length, baseline_dora_path, baseline_random_state_path):
+    """Where condition (start, length) resumes from, by LEN:137-256 / NEWP:1156-1201:
+
+    1. its own results CSV has epochs: continue in place from the last one (its own
+       ``dora_params_{E}`` / ``random_states_{E}``);
+    2. else the longest shorter sibling with the same start (same trajectory through the end of
+       the sibling's window, since the per-batch perturbation seeds depend only on the start
+       epoch and batch): resume at epoch ``start - 1 + sibling_length`` from the sibling's files,
+       with its CSV rows up to there.  A sibling whose files for that epoch are missing (it
+       stopped early) is passed over for the next shorter one -- the reference would fall back
+       to the freshly initialised DoRA parameters there (NEWP:1166-1171);
+    3. else the baseline run at epoch ``start - 1``.
+
+    Returns dict(resume_from_epoch, dora_dir, random_state_dir, previous_csv, source)."""
+    d = condition_dir(out_dir, perturb_type, start, length)
+    own_csv = os.path.join(d, "training_res.csv")
+    own_dora, own_rs = os.path.join(d, f"dora_params_{start}"), os.path.join(d, f"random_states_{start}")
+    last = last_completed_epoch(own_csv)
+    if last > 0:
+        return dict(resume_from_epoch=last, dora_dir=own_dora, random_state_dir=own_rs, previous_csv=own_csv,
+                    source="self")
+    for sib, sib_len in _sibling_candidates(out_dir, perturb_type, start, length):
+        ep = max(0, start - 1) + sib_len
+        sd, sr = os.path.join(sib, f"dora_params_{start}"), os.path.join(sib, f"random_states_{start}")
+        if (os.path.exists(os.path.join(sd, f"epoch{ep}_dora_params.pth"))
+                and os.path.exists(os.path.join(sr, f"epoch{ep}_random_states.pth"))):
+            return dict(resume_from_epoch=ep, dora_dir=sd, random_state_dir=sr,
+                        previous_csv=os.path.join(sib, "training_res.csv"), source=f"sibling l{sib_len}")
+    return dict(resume_from_epoch=max(0, start - 1), dora_dir=baseline_dora_path,
+                random_state_dir=baseline_random_state_path, previous_csv=None, source="baseline")
+
+
 def run_sweep(make_model_and_optimizer, criterion, data, conditions: Sequence[Tuple[int, int]], *, rank=0,
               world=1, perturb_type, out_dir, baseline_dora_path, baseline_random_state_path, epochs,
               **train_kw) -> List[Tuple[Tuple[int, int], str]]:
     """Run this rank's share of ``conditions`` ((training_run, perturb_length) pairs, LEN:42-83).
 
-    Each condition resumes from the baseline run at epoch ``training_run - 1`` (its DoRA file and
-    RNG / optimizer state, NEWP:1157-1201), trains to ``epochs`` with the perturbation window,
-    and writes its CSV / DoRA / RNG files under ``out_dir/run{start}_len{length}``.  No
-    collective: conditions are independent."""
+    ``parallel.shard_conditions`` keeps each start epoch's chain on one rank, and a chain runs in
+    increasing length, so each condition finds its shorter sibling finished (``resume_plan``).
+    Each condition writes LEN's layout: ``out_dir/{perturb_type}_e{E}_l{L}/training_res.csv``,
+    ``dora_params_{E}/``, ``random_states_{E}/``.  No collective: conditions are independent
+    (SURVEY §8e).  Returns [((start, length), csv path, resume source)]."""
     done = []
     for start, length in shard_conditions(conditions, world, rank):
+        plan = resume_plan(out_dir, perturb_type, start, length, baseline_dora_path, baseline_random_state_path)
+        d = condition_dir(out_dir, perturb_type, start, length)
+        res = os.path.join(d, "training_res.csv")
+        if last_completed_epoch(res) >= epochs:
+            done.append(((start, length), res, "complete"))
+            continue
         model, optimizer = make_model_and_optimizer()
         gen = torch.Generator()
-        resume = start - 1
-        if resume > 0:
-            load_dora_parameters(model, baseline_dora_path, resume)
-            load_random_states(baseline_random_state_path, resume, optimizer, gen)
-        d = os.path.join(out_dir, f"run{start}_len{length}")
+        resume = plan["resume_from_epoch"]
+        if resume > 0 and start >= 1:
+            load_dora_parameters(model, plan["dora_dir"], resume)
+            load_random_states(plan["random_state_dir"], resume, optimizer, gen)
         os.makedirs(d, exist_ok=True)
-        res = os.path.join(d, "training_res.csv")
         train_condition(model, optimizer, criterion, data, epochs=epochs, training_run=start, perturb_length=length,
-                        perturb_type=perturb_type, training_res_path=res, dora_parameters_path=os.path.join(d, "dora"),
-                        random_state_path=os.path.join(d, "random_states"), dataloader_generator=gen,
-                        resume_from_epoch=resume, **train_kw)
-        done.append(((start, length), res))
+                        perturb_type=perturb_type, training_res_path=res,
+                        dora_parameters_path=os.path.join(d, f"dora_params_{start}"),
+                        random_state_path=os.path.join(d, f"random_states_{start}"), dataloader_generator=gen,
+                        resume_from_epoch=resume, previous_training_res_path=plan["previous_csv"], **train_kw)
+        done.append(((start, length), res, plan["source"]))
     return done
+
+
+def _sweep_worker(rank, world, make_model_and_optimizer, criterion, data, conditions, kw, results, devices):
+    threads = kw.pop("torch_threads", None)
+    if threads:
+        torch.set_num_threads(threads)
+    if devices:
+        torch.cuda.set_device(devices[rank % len(devices)])
+    out = run_sweep(make_model_and_optimizer, criterion, data, conditions, rank=rank, world=world, **kw)
+    results.put((rank, out))
+
+
+def launch_sweep(nprocs, make_model_and_optimizer, criterion, data, conditions, *, gpus=None, **kw):
+    """One process per GPU (or per CPU worker when ``gpus`` is None), each running its
+    ``shard_conditions`` share of ``conditions`` through :func:`run_sweep` -- the 8-way sharded
+    C5 sweep with no collective.  ``make_model_and_optimizer`` and ``criterion``
+    must be picklable (module-level).  Returns {rank: [((start, length), csv, source)]}."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    devices = list(gpus) if gpus else []
+    procs = [ctx.Process(target=_sweep_worker,
+                         args=(r, nprocs, make_model_and_optimizer, criterion, data, conditions, kw, q, devices))
+             for r in range(nprocs)]
+    for p in procs:
+        p.start()
+    import queue as _queue
+    out = {}
+    try:
+        while len(out) < nprocs:
+            try:
+                r, res = q.get(timeout=1.0)
+                out[r] = res
+            except _queue.Empty:
+                dead = [(i, p.exitcode) for i, p in enumerate(procs) if p.exitcode not in (None, 0) and i not in out]
+                if dead:
+                    raise RuntimeError(f"sweep workers failed (rank, exit code): {dead}")
+    finally:
+        for p in procs:
+            if p.exitcode is None and len(out) < nprocs:
+                p.terminate()
+            p.join()
+    return out
