@@ -140,12 +140,15 @@ int vit_sgd_tensor_bytes(void);
 int vit_sgd_chunk_bytes(void);
 
 /* DoRALayer.weight (NEWP:447-463): W[out,in] = (m * (D + (B@A)s) / (||.||_col + 1e-8))^T,
- * and its backward (dm, dA, dB) for AdamW (NEWP:1000-1001). */
+ * and its backward (dm, dA, dB) for AdamW (NEWP:1000-1001).  noise (nullable, [in,out] like D):
+ * DoRALayer.forward's train-mode dropout of delta_D (NEWP:465-481), (B@A)s * noise with
+ * noise = keep-mask / (1 - p); the backward masks the delta_D gradient the same way. */
 int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, const float* B, const float* D,
-                        float scaling, float* W, float* nu, float* DnT_ws, float* colsq_ws, void* stream);
+                        float scaling, const float* noise, float* W, float* nu, float* DnT_ws, float* colsq_ws,
+                        void* stream);
 int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, const float* B, const float* gW,
                         const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
-                        float* sdDnT_ws, void* unused, void* stream);
+                        float* sdDnT_ws, const float* noise, void* stream);
 /* torch.optim.AdamW step (NEWP:1181, NEWP:1001): tensors {float* p; const float* g; float* exp_avg;
  * float* exp_avg_sq; bf16* shadow (or null); int64 n; float step_size; float bc2_sqrt}[] where
  * step_size = lr / (1 - beta1^step) and bc2_sqrt = sqrt(1 - beta2^step) for that tensor's own

@@ -177,6 +177,39 @@ def dora_fixture():
     return out
 
 
+def dora_forward_fixture():
+    """DoRALayer.forward in train mode (NEWP:465-481: dropout on delta_D) through the reference's own
+    class on CPU, with x / bias gradients.  The dropout noise it drew is recovered by re-seeding and
+    drawing nn.Dropout on ones of delta_D's shape (same RNG consumption); the fixture checks that
+    the reference output equals the noise-multiplier restatement, and stores the noise so the GPU
+    test can feed the identical mask to the HIP kernels."""
+    _stub_reference_imports()
+    import functions.new_cvpr_train_behavior_things_pipeline as NEWP
+    torch.manual_seed(77)
+    base = torch.nn.Linear(96, 80)
+    layer = NEWP.DoRALayer(base, r=8, dora_alpha=16, dora_dropout=0.1)
+    layer.train()
+    x = torch.randn(6, 96, requires_grad=True)
+    gy = torch.randn(6, 80)
+    torch.manual_seed(78)
+    y = layer(x)
+    (y * gy).sum().backward()
+    torch.manual_seed(78)
+    noise = layer.dora_dropout(torch.ones(96, 80))
+    with torch.no_grad():
+        dD = (layer.delta_D_B @ layer.delta_D_A) * layer.scaling * noise
+        Dn = layer.D + dD
+        W = (Dn / (torch.norm(Dn, dim=0, keepdim=True) + 1e-8) * layer.m).T
+        y2 = torch.nn.functional.linear(x, W, layer.bias)
+    assert torch.equal(y2, y.detach()), (y2 - y).abs().max()
+    assert (noise == 0).any() and ((noise == 0) | (noise == noise.max())).all()
+    return {"m": layer.m.detach().clone(), "A": layer.delta_D_A.detach().clone(),
+            "B": layer.delta_D_B.detach().clone(), "D": layer.D.clone(), "bias": layer.bias.detach().clone(),
+            "scaling": layer.scaling, "noise": noise, "x": x.detach().clone(), "gy": gy, "y": y.detach().clone(),
+            "dx": x.grad.clone(), "dm": layer.m.grad.clone(), "dA": layer.delta_D_A.grad.clone(),
+            "dB": layer.delta_D_B.grad.clone(), "dbias": layer.bias.grad.clone()}
+
+
 def rsa_fixture():
     _stub_reference_imports()
     import scipy.io
@@ -386,7 +419,8 @@ def main():
     only = sys.argv[1:]
     if only:  # e.g. `make_golden.py clip perturb`: regenerate just those fixtures
         for name in only:
-            fn = {"clip": (clip_fixture, "clip_golden.pt"), "perturb": (perturb_fixture, "perturb_golden.pt")}[name]
+            fn = {"clip": (clip_fixture, "clip_golden.pt"), "perturb": (perturb_fixture, "perturb_golden.pt"),
+                  "dora_fwd": (dora_forward_fixture, "dora_forward_golden.pt")}[name]
             torch.save(fn[0](), os.path.join(HERE, fn[1]))
         return
     print("ViT tiny fixture")
@@ -395,6 +429,7 @@ def main():
     torch.save(vit_fixture(R.VIT_B16, B=2, seed=0, full_grads=False), os.path.join(HERE, "vit_b16_golden.pt"))
     print("DoRA fixture (reference DoRALayer)")
     torch.save(dora_fixture(), os.path.join(HERE, "dora_golden.pt"))
+    torch.save(dora_forward_fixture(), os.path.join(HERE, "dora_forward_golden.pt"))
     print("RSA fixture (reference behavioral_RSA)")
     np.savez(os.path.join(HERE, "rsa_golden.npz"), **rsa_fixture())
     print("LR fixture (reference CosineAnnealingLRWithWarmup)")

@@ -154,7 +154,12 @@ def test_clip_hba_step_matches_golden(gold, dtype):
     assert _rel(pred, gold["pred"]) < (1e-3 if f32 else 3e-2)
     assert abs(float(loss.detach()) - gold["loss"]) <= (1e-3 if f32 else 3e-2) * abs(gold["loss"])
     for n, g in gold["grads"].items():
-        assert _rel(grads[n], g) < (1e-3 if f32 else 1e-1), (n, _rel(grads[n], g))
+        if f32:
+            assert _rel(grads[n], g) < 1e-3, (n, _rel(grads[n], g))
+        else:  # bf16 opt-in: per-tensor direction and norm
+            a, b = grads[n].flatten().double(), g.flatten().double()
+            cos = torch.nn.functional.cosine_similarity(a, b, dim=0).item()
+            assert cos >= 0.99 and abs(a.norm().item() / b.norm().item() - 1) <= 0.05, (n, cos)
     after = dict(m.named_parameters())
     for n, w in gold["dora_after"].items():
         before = gold["dora_A_init"].get(n) if n.endswith("delta_D_A") else gold["dora_B_init"].get(n)

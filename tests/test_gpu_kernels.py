@@ -158,6 +158,44 @@ def test_gemm_every_tile_config(variant):
         lib.vit_gemm_variant(-1)
 
 
+@pytest.mark.parametrize("M,N,K", [(197 * 3, 640, 448), (1024, 768, 96), (300, 132, 64)])
+def test_f32_mfma_gemm_every_layout_and_epilogue(M, N, K):
+    """The fp32 MFMA kernel (v_mfma_f32_16x16x4_f32; the compute_dtype=float32 path and CLIP at
+    the reference's precision): forward with bias / GELU / QuickGELU / residual epilogues, dgrad
+    with the GELU' epilogue and fused bias column sums, split-K wgrad with a ragged M tail --
+    ragged M / N tiles, against float64 CPU references at 1e-5 of scale."""
+    x = _rnd(M, K, seed=60)
+    w = _rnd(N, K, seed=61, scale=0.05)
+    b = _rnd(N, seed=62)
+    res = _rnd(M, N, seed=63)
+    dy = _rnd(M, N, seed=64)
+    xd, wd, bd, dyd = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV)
+    ref = (x.double() @ w.double().T + b.double()).float()
+    _close(ops.linear_fwd(xd, wd, bd, out_dtype=torch.float32), ref, 1e-5, "fwd")
+    dact, act = ops.linear_fwd(xd, wd, bd, epi=L.EPI_BIAS_GELU, out_dtype=torch.float32)
+    _close(act, torch.nn.functional.gelu(ref), 1e-5, "gelu")
+    _close(dact, _gelu_grad(ref), 1e-5, "gelu'")
+    dq, aq = ops.linear_fwd(xd, wd, bd, epi=L.EPI_BIAS_QGELU, out_dtype=torch.float32)
+    sg = torch.sigmoid(1.702 * ref)
+    _close(aq, ref * sg, 1e-5, "qgelu")
+    out = res.to(DEV).clone()
+    ops.linear_fwd(xd, wd, bd, epi=L.EPI_RESID, resid=out, out=out)
+    _close(out, ref + res, 1e-5, "resid")
+    dref = (dy.double() @ w.double()).float()
+    _close(ops.linear_dgrad(dyd, wd, out_dtype=torch.float32), dref, 1e-5, "dgrad")
+    pre = _rnd(M, K, seed=65)
+    db = torch.empty(K, device=DEV)
+    d = ops.linear_dgrad(dyd, wd, out_dtype=torch.float32, epi=L.EPI_GELU_BWD, pre=pre.to(DEV), dbias=db)
+    _close(d, dref * pre, 1e-5, "gelu bwd")
+    _close(db, (dref.double() * pre.double()).sum(0).float(), 1e-5, "fused dbias")
+    wref = (dy.double().T @ x.double()).float()
+    for split in (1, 3):
+        _close(ops.linear_wgrad(dyd, xd, split=split), wref, 1e-5, f"wgrad split {split}")
+    tail = M - 5  # ragged reduction tail (M % 32 != 0) through the generic kernel
+    _close(ops.linear_wgrad(dyd[:tail], xd[:tail], split=2), (dy[:tail].double().T @ x[:tail].double()).float(),
+           1e-5, "wgrad ragged")
+
+
 @pytest.mark.parametrize("K", [448, 768])
 def test_gemm_persistent_many_tiles(K):
     """The persistent forward / dgrad kernel (variant 10) with more tiles than CUs, so the
@@ -518,6 +556,50 @@ def test_fused_adamw_update_reaches_bf16_forward():
     with torch.no_grad():
         fresh = m2(x)
     assert torch.equal(after, fresh)
+
+
+def test_dora_forward_train_dropout_matches_reference_fixture(golden_dir):
+    """DoRALayer.forward in train mode (NEWP:465-481: dropout on delta_D, then F.linear) on the HIP
+    kernels with the reference's recorded dropout noise: output and every gradient (x, m, A, B,
+    bias) against the reference class run on CPU (dora_forward_golden.pt, make_golden.py)."""
+    import vit_amd
+    from vit_amd.dora import _LinearF32Fn
+    fx = torch.load(os.path.join(golden_dir, "dora_forward_golden.pt"), weights_only=True)
+    m = fx["m"].clone().to(DEV).requires_grad_(True)
+    A = fx["A"].clone().to(DEV).requires_grad_(True)
+    Bm = fx["B"].clone().to(DEV).requires_grad_(True)
+    b = fx["bias"].clone().to(DEV).requires_grad_(True)
+    x = fx["x"].clone().to(DEV).requires_grad_(True)
+    W = vit_amd.dora_weight(m, A, Bm, fx["D"].to(DEV), fx["scaling"], fx["noise"].to(DEV))
+    y = _LinearF32Fn.apply(x, W, b)
+    _close(y, fx["y"], 1e-5, "y")
+    y.backward(fx["gy"].to(DEV))
+    for t, k in ((x, "dx"), (m, "dm"), (A, "dA"), (Bm, "dB"), (b, "dbias")):
+        _close(t.grad, fx[k], 1e-4, k)
+
+
+def test_dora_layer_forward_train_mode_draws_the_reference_mask():
+    """The module path: DoRALayer.forward in train mode on the GPU draws its dropout with the
+    same RNG consumption as the reference's ``self.dora_dropout(delta_D)`` (same shape, device and
+    generator state), so re-seeding and running the reference's forward in torch on the GPU gives
+    the same output; eval mode (and p = 0) is ``F.linear(x, weight, bias)``."""
+    import vit_amd
+    torch.manual_seed(5)
+    base = torch.nn.Linear(64, 48)
+    layer = vit_amd.DoRALayer(base, r=4, dora_alpha=16, dora_dropout=0.1).to(DEV).train()
+    x = torch.randn(7, 64, device=DEV)
+    torch.cuda.manual_seed(9)
+    y = layer(x)
+    torch.cuda.manual_seed(9)
+    with torch.no_grad():
+        dD = layer.dora_dropout((layer.delta_D_B @ layer.delta_D_A) * layer.scaling)
+        Dn = layer.D + dD
+        Wr = (Dn / (torch.norm(Dn, dim=0, keepdim=True) + 1e-8) * layer.m).T
+        yr = torch.nn.functional.linear(x, Wr, layer.bias)
+    _close(y, yr, 1e-5, "train forward")
+    layer.eval()
+    with torch.no_grad():
+        _close(layer(x), torch.nn.functional.linear(x, layer.weight, layer.bias), 1e-5, "eval forward")
 
 
 def test_dora_weight_matches_reference_fixture(golden_dir):

@@ -121,3 +121,17 @@ def test_sgd_restatement_matches_torch():
         opt.step()
         for k in p:
             torch.testing.assert_close(p[k], q[k].detach(), rtol=1e-6, atol=1e-7)
+
+
+def test_dora_forward_fixture_is_the_noise_restatement(golden_dir):
+    """dora_forward_golden.pt (the reference DoRALayer.forward in train mode, NEWP:465-481) equals
+    W = m * (D + (B@A)s * noise) / (||.||_col + 1e-8), y = x W^T + b with the recorded noise --
+    the restatement the HIP kernels implement (tests/test_gpu_kernels.py feeds them this noise)."""
+    import torch
+    fx = torch.load(os.path.join(golden_dir, "dora_forward_golden.pt"), weights_only=True)
+    dD = (fx["B"] @ fx["A"]) * fx["scaling"] * fx["noise"]
+    Dn = fx["D"] + dD
+    W = (Dn / (torch.norm(Dn, dim=0, keepdim=True) + 1e-8) * fx["m"]).T
+    assert torch.equal(torch.nn.functional.linear(fx["x"], W, fx["bias"]), fx["y"])
+    keep = fx["noise"] != 0
+    assert 0.8 < keep.float().mean().item() < 0.97 and torch.allclose(fx["noise"][keep], torch.tensor(1 / 0.9))

@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.join(ROOT, "vit-project_amd"))
 import torch  # noqa: E402
 
 PEAK = 256 * 4 * 1024 * 2.4e9 / 1e12
+PEAK_F32 = 256 * 4 * 64 * 2.4e9 / 1e12  # v_mfma_f32_16x16x4_f32 / VALU FMA: 64 FLOP/clk/SIMD
 
 
 def block_flops(tokens, width, seq, heads_dim=64):
@@ -37,11 +38,14 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--dtype", choices=["f32", "bf16"], default="f32",
+                    help="compute dtype: f32 = the reference's precision (NEWP:274), bf16 opt-in")
     a = ap.parse_args()
     import vit_amd
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    m = vit_amd.CLIPHBA(["class%d" % i for i in range(66)], "ViT-L/14", pos_embedding=True)
+    T = torch.float32 if a.dtype == "f32" else torch.bfloat16
+    m = vit_amd.CLIPHBA(["class%d" % i for i in range(66)], "ViT-L/14", pos_embedding=True, compute_dtype=T)
     vit_amd.apply_dora_to_ViT(m, n_vision_layers=2, n_transformer_layers=1, r=32)
     vit_amd.switch_dora_layers(m, freeze_all=True, dora_state=True)
     m = m.to(dev)
@@ -74,9 +78,10 @@ def main():
     tf = step_flop * a.steps / el / 1e12
     print(json.dumps({"metric": "images/sec CLIP-HBA ViT-L/14 + DoRA train step (config C3)", "value": round(ips, 2),
                       "unit": "images/s", "ms_per_step": round(el / a.steps * 1e3, 3), "batch": B,
-                      "dtype": "bf16", "data": "synthetic images / targets, random-init weights",
+                      "dtype": a.dtype, "data": "synthetic images / targets, random-init weights",
                       "step_tflop": round(step_flop / 1e12, 3), "achieved_tflops": round(tf, 1),
-                      "frac_of_bf16_peak": round(tf / PEAK, 4), "final_loss": round(float(loss.item()), 4)}))
+                      "peak_tflops": PEAK if a.dtype == "bf16" else PEAK_F32,
+                      "frac_of_peak": round(tf / (PEAK if a.dtype == "bf16" else PEAK_F32), 4), "final_loss": round(float(loss.item()), 4)}))
 
 
 if __name__ == "__main__":

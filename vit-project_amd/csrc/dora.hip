@@ -24,7 +24,8 @@ constexpr int DT = 64;
 
 __global__ __launch_bounds__(256) void dora_tile_kernel(int in, int out, int r, const float* __restrict__ A,
                                                         const float* __restrict__ Bm, const float* __restrict__ D,
-                                                        float s, float* __restrict__ DnT, float* __restrict__ colsq) {
+                                                        float s, const float* __restrict__ noise,
+                                                        float* __restrict__ DnT, float* __restrict__ colsq) {
   __shared__ float Bs[DT][65], As[64][DT + 1], T[DT][DT + 1];
   __shared__ float red[4][DT];
   const int i0 = blockIdx.y * DT, o0 = blockIdx.x * DT, t = threadIdx.x;
@@ -41,7 +42,12 @@ __global__ __launch_bounds__(256) void dora_tile_kernel(int in, int out, int r, 
     int il = ig * 16 + u, i = i0 + il, o = o0 + ol;
     float acc = 0.f;
     for (int k = 0; k < r; ++k) acc = fmaf(Bs[il][k], As[k][ol], acc);
-    float dn = (i < in && o < out) ? D[(int64_t)i * out + o] + acc * s : 0.f;
+    float dn = 0.f;
+    if (i < in && o < out) {
+      const int64_t e = (int64_t)i * out + o;
+      // DoRALayer.forward (NEWP:467-470): dropout(delta_D) = (B@A * s) * noise, noise = mask / (1 - p)
+      dn = D[e] + (noise ? (acc * s) * noise[e] : acc * s);
+    }
     T[ol][il] = dn;
     sq += dn * dn;
   }
@@ -71,7 +77,8 @@ __global__ __launch_bounds__(256) void dora_finish_kernel(int in, int out, int n
 // one wave per row o: c = gW[o].DnT[o]; dm; sdDnT[o][:] = s * dDn^T
 __global__ __launch_bounds__(256) void dora_bwd_row_kernel(int in, int out, const float* __restrict__ gW,
                                                            const float* __restrict__ DnT, const float* __restrict__ m,
-                                                           const float* __restrict__ nu, float s, float* __restrict__ dm,
+                                                           const float* __restrict__ nu, float s,
+                                                           const float* __restrict__ noise, float* __restrict__ dm,
                                                            float* __restrict__ sdDnT) {
   int o = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (o >= out) return;
@@ -83,7 +90,8 @@ __global__ __launch_bounds__(256) void dora_bwd_row_kernel(int in, int out, cons
   const float a = mo / n, bcoef = (v > 0.f) ? mo * c / (n * n * v) : 0.f;
   for (int i = lane; i < in; i += 64) {
     int64_t e = (int64_t)o * in + i;
-    sdDnT[e] = s * (a * gW[e] - bcoef * DnT[e]);
+    const float g = s * (a * gW[e] - bcoef * DnT[e]);
+    sdDnT[e] = noise ? g * noise[(int64_t)i * out + o] : g;
   }
 }
 
@@ -123,12 +131,13 @@ extern "C" {
 // W [out, in] (f32) from DoRA parameters; DnT_ws >= out*in floats (kept for the
 // backward), colsq_ws >= ceil(in/64)*out floats, nu [out] saved for backward.
 int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, const float* Bm, const float* D,
-                        float scaling, float* W, float* nu, float* DnT_ws, float* colsq_ws, void* stream) {
+                        float scaling, const float* noise, float* W, float* nu, float* DnT_ws, float* colsq_ws,
+                        void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (r > 64 || in <= 0 || out <= 0) return (int)hipErrorInvalidValue;
   int ty = (in + DT - 1) / DT;
   hipLaunchKernelGGL(dora_tile_kernel, dim3((out + DT - 1) / DT, ty), dim3(256), 0, s, in, out, r, A, Bm, D, scaling,
-                     DnT_ws, colsq_ws);
+                     noise, DnT_ws, colsq_ws);
   VIT_CHECK_LAUNCH();
   hipLaunchKernelGGL(dora_finish_kernel, dim3((out + 3) / 4), dim3(256), 0, s, in, out, ty, colsq_ws, m, DnT_ws, W, nu);
   VIT_CHECK_LAUNCH();
@@ -139,11 +148,10 @@ int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, 
 // sdDnT_ws >= out*in floats.  Outputs dm [out], dA [r, out], dB [in, r] (f32, overwritten).
 int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, const float* Bm, const float* gW,
                         const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
-                        float* sdDnT_ws, void* unused, void* stream) {
-  (void)unused;
+                        float* sdDnT_ws, const float* noise, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(dora_bwd_row_kernel, dim3((out + 3) / 4), dim3(256), 0, s, in, out, gW, DnT, m, nu, scaling, dm,
-                     sdDnT_ws);
+  hipLaunchKernelGGL(dora_bwd_row_kernel, dim3((out + 3) / 4), dim3(256), 0, s, in, out, gW, DnT, m, nu, scaling,
+                     noise, dm, sdDnT_ws);
   VIT_CHECK_LAUNCH();
   // dB[i][k] = sum_o sdDnT[o][i] * A[k][o]:  P(i,o) = sdDnT[o*in + i] (CR), Q(k,o) = A[k*out + o] (RC)
   int rc = vit_gemm(VIT_F32, VIT_F32, 1, 0, 0, in, r, out, sdDnT_ws, in, A, out, dB, r, nullptr, nullptr, 0, nullptr, 0,

@@ -880,6 +880,7 @@ using V4 = Cfg<256, 128, 32, 4, 2, 4, false, 4>;  //  96 KiB, 1 WG/CU, 4-deep ri
 }  // namespace big
 
 #include "pgemm.inc"
+#include "gemm_f32.inc"
 
 // ----------------------------------------------------------------------------
 // Generic strided kernel: any M, N, R; f32 or bf16 inputs; fp32 FMA.
@@ -998,6 +999,25 @@ static bool fast_ok(int dtype, int pl, int ql, int M, int N, int R, const void* 
   return true;
 }
 
+// fp32 MFMA path (f32m::gemm_kernel): 16-B aligned operands, 4-element row strides, reduction a
+// multiple of 32; a CR operand loads 4-wide column chunks (its extent a multiple of 4).
+static bool fast_f32_ok(int dtype, int pl, int ql, int M, int N, int R, const void* P, const void* Q, int64_t ldp,
+                        int64_t ldq) {
+  if (dtype != VIT_F32) return false;
+  if ((pl == LAY_CR && M % 4) || (ql == LAY_CR && N % 4) || N % 4 || R % f32m::BK || R <= 0) return false;
+  if ((ldp % 4) || (ldq % 4)) return false;
+  if (((uintptr_t)P & 15) || ((uintptr_t)Q & 15)) return false;
+  return true;
+}
+// small grids (the 256-row classifier head) keep the generic kernel's 32x32 tiles: more workgroups
+static bool f32_grid_ok(int M, int N, int split) {
+  return (int64_t)((M + f32m::BM - 1) / f32m::BM) * ((N + f32m::BN - 1) / f32m::BN) * (split > 1 ? split : 1) >= 64;
+}
+static bool any_fast_ok(int dtype, int pl, int ql, int M, int N, int R, const void* P, const void* Q, int64_t ldp,
+                        int64_t ldq) {
+  return fast_ok(dtype, pl, ql, M, N, R, P, Q, ldp, ldq) || fast_f32_ok(dtype, pl, ql, M, N, R, P, Q, ldp, ldq);
+}
+
 static int g_variant = -1;  // -1: per-shape choice; 1, 2, 5: force big::V<n>, 8, 9: ping-pong (tuning)
 static int g_dbg = 0;
 
@@ -1113,6 +1133,24 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
   }
 }
 
+template <int PL, int QL, int EPI, typename TO>
+static int launch_f32(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
+                      const Epi& e, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)f32m::gemm_kernel<PL, QL, EPI, TO, float>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, f32m::LDS);
+    attr = true;
+  }
+  const int r_chunk = r_chunk_for(R, split, f32m::BK);
+  const int nz = (R + r_chunk - 1) / r_chunk;
+  dim3 grid(((M + f32m::BM - 1) / f32m::BM) * ((N + f32m::BN - 1) / f32m::BN) * nz);
+  hipLaunchKernelGGL((f32m::gemm_kernel<PL, QL, EPI, TO, float>), grid, dim3(f32m::THREADS), f32m::LDS, s,
+                     (const float*)P, ldp, (const float*)Q, ldq, M, N, R, r_chunk, e);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename T, int EPI, typename TO, typename TA>
 static int launch_gen(const void* P, int64_t sPi, int64_t sPr, const void* Q, int64_t sQj, int64_t sQr,
                       int M, int N, int R, int split, const Epi& e, hipStream_t s) {
@@ -1165,6 +1203,13 @@ static int gemm_dispatch(int dtype, int out_dtype, int pl, int ql, int M, int N,
     if (pl == LAY_CR && ql == LAY_CR) { FAST(LAY_CR, LAY_CR) }
     if (pl == LAY_CR && ql == LAY_RC) { FAST(LAY_CR, LAY_RC) }
 #undef FAST
+  }
+  if (allow_fast && out_dtype == VIT_F32 && fast_f32_ok(dtype, pl, ql, M, N, R, P, Q, ldp, ldq) && (e.ldc % 4 == 0) &&
+      ((uintptr_t)e.C & 15) == 0 && f32_grid_ok(M, N, split)) {
+    if (pl == LAY_RC && ql == LAY_RC) return launch_f32<LAY_RC, LAY_RC, EPI, float>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    if (pl == LAY_RC && ql == LAY_CR) return launch_f32<LAY_RC, LAY_CR, EPI, float>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    if (pl == LAY_CR && ql == LAY_CR) return launch_f32<LAY_CR, LAY_CR, EPI, float>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    return launch_f32<LAY_CR, LAY_RC, EPI, float>(P, ldp, Q, ldq, M, N, R, split, e, s);
   }
   int64_t sPi = pl == LAY_RC ? ldp : 1, sPr = pl == LAY_RC ? 1 : ldp;
   int64_t sQj = ql == LAY_RC ? ldq : 1, sQr = ql == LAY_RC ? 1 : ldq;
@@ -1238,7 +1283,8 @@ int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, con
   Epi e = make_epi();
   e.C = dX; e.ldc = lddx; e.aux = pre; e.ld_aux = lddx;
   const int rows = (M + 63) / 64;
-  const bool fast = fast_ok(dtype, LAY_RC, LAY_CR, M, K, N, dY, W, lddy, K) && (lddx % 4 == 0);
+  const bool fast = any_fast_ok(dtype, LAY_RC, LAY_CR, M, K, N, dY, W, lddy, K) && (lddx % 4 == 0) &&
+                    (dtype == VIT_BF16 || (out_dtype == VIT_F32 && ((uintptr_t)dX & 15) == 0 && f32_grid_ok(M, K, 1)));
   if (dbias) {
     if (partial == nullptr || partial_floats < vit_linear_dgrad_partial_floats(M, K)) return (int)hipErrorInvalidValue;
     if (fast) e.csum = partial;
@@ -1288,7 +1334,8 @@ int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t ldd
   if (M <= 0) return (int)hipMemsetAsync(dW, 0, (size_t)N * K * 4, s);
   // the MFMA kernel takes the BK-aligned rows; a ragged tail (M % 32) is added by the generic kernel
   const int tail = M % 32;
-  const bool fast = (M - tail) > 0 && fast_ok(dtype, LAY_CR, LAY_CR, N, K, M - tail, dY, X, lddy, ldx);
+  const bool fast = (M - tail) > 0 && any_fast_ok(dtype, LAY_CR, LAY_CR, N, K, M - tail, dY, X, lddy, ldx) &&
+                    (dtype == VIT_BF16 || (((uintptr_t)dW & 15) == 0 && f32_grid_ok(N, K, split)));
   const int R0 = fast ? M - tail : M;
   if (split > 1 && (workspace == nullptr || ws_bytes < (int64_t)split * N * K * 4)) return (int)hipErrorInvalidValue;
   Epi e = make_epi();
@@ -1298,7 +1345,7 @@ int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t ldd
     rc = gemm_any(EPI_STORE, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, R0, dY, lddy, X, ldx, 1, e, s, fast);
   } else {
     e.C = workspace; e.ldc = K; e.slab = (int64_t)N * K;
-    const int r_chunk = r_chunk_for(R0, split, fast ? 64 : gen::TK);
+    const int r_chunk = r_chunk_for(R0, split, fast ? (dtype == VIT_BF16 ? 64 : f32m::BK) : gen::TK);
     const int nz = (R0 + r_chunk - 1) / r_chunk;
     rc = gemm_any(EPI_STORE, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, R0, dY, lddy, X, ldx, split, e, s, fast);
     if (rc) return rc;

@@ -54,7 +54,7 @@ SIGNATURES = {
     "vit_sgd_chunk_bytes": [],
     "vit_cast_f32_bf16": [vp, vp, i64, vp],
     "vit_zero": [vp, i64, vp],
-    "vit_dora_weight_fwd": [i32, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp],
+    "vit_dora_weight_fwd": [i32, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp],
     "vit_dora_weight_bwd": [i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp],
     "vit_adamw_step": [vp, vp, i32, f32, f32, f32, f32, vp],
     "vit_adamw_tensor_bytes": [],

@@ -21,6 +21,10 @@ dropping the visual positional embedding.  Pretrained weights come from a networ
 the reference (``load_clip_to_cpu``, NEWP:251-265): offline the model is random-initialised,
 or built from a local OpenAI state dict with :func:`build_model`.
 
+Precision: ``compute_dtype=torch.float32`` by default, as the reference runs CLIP
+(``self.clip_model.float()``, NEWP:274, no autocast on this path); ``torch.bfloat16`` is an
+explicit opt-in (bf16 GEMM operands and activations, f32 accumulation and LayerNorm statistics).
+
 Compute: every tower block is the same ``_BlockFn`` as the ViT path (MFMA GEMMs with QuickGELU
 epilogues, LDS-resident attention with a causal flag, wave-per-row LayerNorm).  Only the DoRA
 blocks are autograd nodes with parameters that need gradients; their backward runs just the
@@ -229,7 +233,7 @@ class CLIP(nn.Module):
 
     def __init__(self, embed_dim=768, image_resolution=224, vision_layers=24, vision_width=1024, vision_patch_size=14,
                  context_length=77, vocab_size=49408, transformer_width=768, transformer_heads=12,
-                 transformer_layers=12, compute_dtype=torch.bfloat16, cache_frozen_text=True):
+                 transformer_layers=12, compute_dtype=torch.float32, cache_frozen_text=True):
         super().__init__()
         if vision_width % 64 or transformer_width % 64:
             raise ValueError("the HIP attention kernels require head_dim 64")
@@ -384,7 +388,7 @@ _BACKBONES = {
 }
 
 
-def build_model(state_dict, compute_dtype=torch.bfloat16):
+def build_model(state_dict, compute_dtype=torch.float32):
     """``clip.build_model`` for ViT backbones: dimensions inferred from an OpenAI state dict."""
     vw = state_dict["visual.conv1.weight"].shape[0]
     vl = len({k.split(".")[3] for k in state_dict if k.startswith("visual.transformer.resblocks.")})
@@ -422,7 +426,7 @@ class CLIPHBA(nn.Module):
     ``backbone_name`` and :func:`tokenize` ids are used (no network)."""
 
     def __init__(self, classnames, backbone_name="ViT-L/14", pos_embedding=False, clip_model=None,
-                 tokenized_prompts=None, compute_dtype=torch.bfloat16):
+                 tokenized_prompts=None, compute_dtype=torch.float32):
         super().__init__()
         self.num_clip = len(classnames)
         if clip_model is None:
