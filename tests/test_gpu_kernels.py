@@ -130,7 +130,7 @@ def test_linear_wgrad(M, N, K, split):
     _close(dw, ref, 2e-5, "wgrad")
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 8, 9, 10])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_gemm_every_tile_config(variant):
     """Every kept MFMA configuration (forced through vit_gemm_variant) on ragged
     M/N tiles, fwd + bias/GELU/residual epilogues, dgrad, split-K wgrad."""

@@ -410,8 +410,12 @@ __device__ __forceinline__ void epi1(const Epi& e, int i, int j, float v) {
 // ----------------------------------------------------------------------------
 namespace big {
 
-template <int BM_, int BN_, int BK_, int WI_, int WJ_, int S_, bool DB_, int OCC_> struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, BK = BK_, WI = WI_, WJ = WJ_, STAGES = S_, OCC = OCC_;
+// EPS (epilogue style): 0 = per-shape choice (LDS-staged row-contiguous stores for the bf16 256x256
+// tile and the GELU epilogues), 1 = straight from the MFMA fragments (permlane16-widened 16-B bf16
+// stores, 16-B f32 stores) -- no LDS, so the kernel's LDS is its ring alone and two workgroups
+// share a CU: one's epilogue runs beside the other's MFMAs.
+template <int BM_, int BN_, int BK_, int WI_, int WJ_, int S_, bool DB_, int OCC_, int EPS_ = 0> struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, BK = BK_, WI = WI_, WJ = WJ_, STAGES = S_, OCC = OCC_, EPS = EPS_;
   static constexpr bool DB = DB_;
   static constexpr int WAVES = WI * WJ, THREADS = WAVES * 64;
   static constexpr int WM = BM / WI, WN = BN / WJ;
@@ -657,13 +661,16 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
   // 256x256 tile and the GELU / GELU' epilogues are faster through the row-contiguous LDS
   // staging (tools/bench_kernels.py --sweep: v vs 6400 + v).  Timing flags: dbg 64 forces the
   // staged epilogue, dbg 8 the plain fragment-layout one below (8-B stores).
-  if constexpr (sizeof(TO) == 2 && EPI == EPI_STORE && C::BM * C::BN < 256 * 256) {
+  if constexpr (sizeof(TO) == 2 && ((EPI == EPI_STORE && C::BM * C::BN < 256 * 256) ||
+                                     (C::EPS == 1 && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU ||
+                                                      EPI == EPI_BIAS_QGELU || EPI == EPI_GELU_BWD ||
+                                                      EPI == EPI_QGELU_BWD)))) {
     if (!(e.dbg & (8 | 64)) && N % 32 == 0) {
       epilogue_swap<C, EPI, TO, TA>(e, acc, i0, j0, wi, wj, lane, M, N);
       return;
     }
   }
-  if constexpr (sizeof(TO) == 2) {
+  if constexpr (sizeof(TO) == 2 && C::EPS == 0) {
     if (!(e.dbg & 8)) {
       epilogue_staged<C, EPI, TO, TA>(e, acc, smem, i0, j0, wi, wj, lane, M, N, z);
       return;
@@ -877,6 +884,10 @@ using V2 = Cfg<128, 128, 64, 2, 2, 2, false, 2>;  //  64 KiB, 2 WG/CU (4 waves):
 using V5 = Cfg<256, 256, 64, 2, 4, 2, false, 2>;  // 128 KiB, 1 WG/CU: wide forward, wgrad
 using V3 = Cfg<128, 256, 32, 2, 2, 3, false, 2>;  //  72 KiB, 2 WG/CU (4 waves of 64x128)
 using V4 = Cfg<256, 128, 32, 4, 2, 4, false, 4>;  //  96 KiB, 1 WG/CU, 4-deep ring
+// 4 waves of 128x64 (V5's wave tile), 3-deep ring, epilogue from the fragments: 72 KiB -> 2
+// workgroups per CU (one wave per SIMD each), whose epilogues overlap each other's MFMAs
+using V6 = Cfg<256, 128, 32, 2, 2, 3, false, 2, 1>;
+using V7 = Cfg<128, 256, 32, 2, 2, 3, false, 2, 1>;  // 4 waves of 64x128
 }  // namespace big
 
 #include "pgemm.inc"
@@ -1042,7 +1053,7 @@ static int r_chunk_for(int R, int split, int bk) {
 template <class C, int PL, int QL, int EPI, typename TO, typename TA>
 static int launch_big(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
                       const Epi& e, hipStream_t s) {
-  constexpr int lds = C::LDS > EpiLds<C, TO>::BYTES ? C::LDS : EpiLds<C, TO>::BYTES;
+  constexpr int lds = (C::EPS == 1 || C::LDS > EpiLds<C, TO>::BYTES) ? C::LDS : EpiLds<C, TO>::BYTES;
   static_assert(lds <= 163840, "LDS");
   static bool attr = false;
   if (!attr) {
@@ -1127,6 +1138,8 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
     case 5: return launch_big<big::V5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 3: return launch_big<big::V3, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 4: return launch_big<big::V4, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    case 6: return launch_big<big::V6, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    case 7: return launch_big<big::V7, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 8: return launch_pp<4, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 9: return launch_pp<5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     default: return launch_big<big::V1, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);

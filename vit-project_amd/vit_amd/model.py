@@ -76,6 +76,8 @@ _HOLD_REFS = [os.environ.get("VIT_HOLD_REFS", "1") != "0"]
 # ~0.3 ms later (bs=256).  Default B/32 (8 at bs=256): +0.8 %; 16+ falls off a GEMM tile-count
 # cliff (-3 %).  profiles/r01/ab_fwd_half_split.json
 _FWD_HALF_DELTA = [None if os.environ.get("VIT_FWD_HALF_DELTA") is None else int(os.environ["VIT_FWD_HALF_DELTA"])]
+# forward: launches of each block the caller's chain queues before the side chain is released
+_FWD_STAGGER = [int(os.environ.get("VIT_FWD_STAGGER", "0"))]
 _HOLD = {}
 
 
@@ -271,32 +273,45 @@ class _BlockFn(torch.autograd.Function):
         causal = bool(cfg.get("causal", False))
 
         def chain(b0, b1):
-            """The block over images [b0, b1): rows b0*N .. b1*N of every tensor."""
+            """The block over images [b0, b1) (rows b0*N .. b1*N of every tensor) as its 7 launches."""
             r0, r1_ = b0 * N, b1 * N
             sl = slice(r0, r1_)
-            ops.layer_norm_fwd(x2[sl], n1w.detach(), n1b.detach(), eps, T, out=h1[sl], mean=m1[sl], rstd=r1[sl])
-            ops.linear_fwd(h1[sl], Wqkv, qkvb.detach(), out=qkv[sl])
-            ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N], causal=causal)
-            ops.linear_fwd(o[sl], Wproj, projb.detach(), epi=L.EPI_RESID, resid=x2[sl], out=xm[sl])
-            ops.layer_norm_fwd(xm[sl], n2w.detach(), n2b.detach(), eps, T, out=h2[sl], mean=m2[sl], rstd=r2[sl])
-            ops.linear_fwd(h2[sl], W1, fc1b.detach(), epi=act_epi, out=dact[sl], act_out=act[sl])
-            ops.linear_fwd(act[sl], W2, fc2b.detach(), epi=L.EPI_RESID, resid=xm[sl], out=xo[sl])
+            return [
+                lambda: ops.layer_norm_fwd(x2[sl], n1w.detach(), n1b.detach(), eps, T, out=h1[sl], mean=m1[sl],
+                                           rstd=r1[sl]),
+                lambda: ops.linear_fwd(h1[sl], Wqkv, qkvb.detach(), out=qkv[sl]),
+                lambda: ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N], causal=causal),
+                lambda: ops.linear_fwd(o[sl], Wproj, projb.detach(), epi=L.EPI_RESID, resid=x2[sl], out=xm[sl]),
+                lambda: ops.layer_norm_fwd(xm[sl], n2w.detach(), n2b.detach(), eps, T, out=h2[sl], mean=m2[sl],
+                                           rstd=r2[sl]),
+                lambda: ops.linear_fwd(h2[sl], W1, fc1b.detach(), epi=act_epi, out=dact[sl], act_out=act[sl]),
+                lambda: ops.linear_fwd(act[sl], W2, fc2b.detach(), epi=L.EPI_RESID, resid=xm[sl], out=xo[sl]),
+            ]
+
+        def run(steps):
+            for f in steps:
+                f()
 
         side = _Side(dev)
         if side.on and B >= 2 and T != torch.float32:
             # two half-batch chains on two streams: one chain's GEMM epilogues (HBM-bound)
-            # overlap the other's MFMA main loops
+            # overlap the other's MFMA main loops.  The side chain is released (side.run waits for
+            # everything the caller's stream has queued) after the caller's first _FWD_STAGGER
+            # launches of this block, so the two chains run out of phase by that many kernels.
             delta = B // 32 if _FWD_HALF_DELTA[0] is None else _FWD_HALF_DELTA[0]
             hb = min(B - 1, max(1, B // 2 + delta))
-            side.run(lambda: chain(hb, B))
+            mine, other = chain(0, hb), chain(hb, B)
+            k = max(0, min(len(mine), _FWD_STAGGER[0]))
+            run(mine[:k])
+            side.run(lambda: run(other))
             side.guard(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act, xo)
-            chain(0, hb)
+            run(mine[k:])
             # each half only feeds the same half of the next block: a stack of blocks joins
             # once after its last block (cfg "defer_join", ViT._tokens) instead of per block
             if not cfg.get("defer_join"):
                 side.join()
         else:
-            chain(0, B)
+            run(chain(0, B))
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act)
         ctx.params = (n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.wops = (Wqkv, Wproj, W1, W2)
