@@ -115,6 +115,13 @@ int vit_layer_norm_bwd_blocks(int rows); /* partial rows: the [nblk][D] partial 
  * tower's nn.MultiheadAttention attn_mask (NEWP:298 through the CLIP-HBA fork, external). */
 int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, void* o,
                  int64_t ld_o, float* lse, float scale, int causal, void* stream);
+/* fp8 scaled-dot-product attention forward (BASELINE configs[4]: the sweep's frozen CLIP tower blocks
+ * and the RSA evaluation forward; replaces the same F.scaled_dot_product_attention call as
+ * vit_sdpa_fwd): q/k/v quantised in-kernel to block-scaled OCP e4m3 (E8M0 scale per 32 values),
+ * S = QK^T and O = PV on v_mfma_scale_f32_32x32x64_f8f6f4, softmax in f32.  dtype = qkv/o dtype
+ * (VIT_BF16 or VIT_F32); head_dim 64, N <= 320; lse may be null.  Forward only. */
+int vit_sdpa_fwd_fp8(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, void* o,
+                     int64_t ld_o, float* lse, float scale, int causal, void* stream);
 /* SDPA backward into dqkv (qkv layout). delta_ws >= B*H*N floats.  dbias (optional, [3*H*64]) =
  * column sums of dqkv (the qkv Linear's bias gradient), fused into the kernels;
  * partial >= vit_sdpa_bwd_partial_floats(B, N, H*64). */

@@ -135,3 +135,21 @@ def test_dora_forward_fixture_is_the_noise_restatement(golden_dir):
     assert torch.equal(torch.nn.functional.linear(fx["x"], W, fx["bias"]), fx["y"])
     keep = fx["noise"] != 0
     assert 0.8 < keep.float().mean().item() < 0.97 and torch.allclose(fx["noise"][keep], torch.tensor(1 / 0.9))
+
+
+def test_fp8_attention_restatement_known_answers():
+    """oracle/attn_fp8_ref.py: E8M0 block exponents (smallest e with amax <= 448 * 2^e), e4m3
+    rounding, and the restated fp8 attention's distance from exact attention on random inputs."""
+    import torch
+    from oracle import attn_fp8_ref as F8
+    a = torch.tensor([448.0, 449.0, 1.0, 0.0, 1e-30, 1.75 * 2 ** 11, 1.76 * 2 ** 11])
+    assert F8.e8m0_exp(a).tolist() == [0, 1, -8, -127, -108, 3, 4]
+    x = torch.tensor([[1.0, 0.1, 447.0, 3.3] * 16])
+    xq = F8.quant_rows(x)
+    assert xq[0, 0] == 1.0 and xq[0, 2] == 448.0 and abs(xq[0, 1] - 0.1) < 0.0079
+    g = torch.Generator().manual_seed(0)
+    q, k, v = (torch.randn(1, 2, 197, 64, generator=g) for _ in range(3))
+    o, lse = F8.sdpa_fp8(q, k, v)
+    ex = F8.exact_sdpa(q, k, v)
+    assert (o - ex).abs().max() / ex.abs().max() < 0.12
+    assert torch.nn.functional.cosine_similarity(o.flatten(), ex.flatten(), dim=0) > 0.997

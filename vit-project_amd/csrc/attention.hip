@@ -186,6 +186,225 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// fp8 forward (BASELINE configs[4]: the perturbation sweep's frozen-tower attention and the RSA
+// evaluation forward).  Block-scaled OCP e4m3 operands on v_mfma_scale_f32_32x32x64_f8f6f4
+// (twice the bf16 MFMA rate per clock), operand layouts probed with exact one-hot data
+// (tools/probe/mfma_scale_probe.hip): lane l holds A[row l%32][k = 32(l/32) + byte] and
+// B[k = 32(l/32) + byte][col l%32]; its E8M0 scale byte covers those 32 k values.
+//
+//   S^T = K Q^T: A = K (rows = keys, k = d), B = Q^T; one MFMA per 32-key tile (hd = 64 = K).
+//     Q and K are quantised per row (all 64 d): e = the smallest exponent with
+//     max|x| <= 448 * 2^e, byte = x * 2^-e rounded to e4m3, E8M0 scale 127 + e in both lane halves
+//     of the row.  (One scale per row, not per 32 values: the hardware's 32-value scale blocks
+//     interleave the two lane halves' bytes -- tools/probe/mfma_scale_probe.hip, test 6.)
+//   P = exp(S - rowmax) in (0, 1], quantised as P * 2^8 (scale 2^-8): no block max needed.
+//   O^T = V^T P^T: A = V^T (rows = d, k = keys), B = P^T straight from the S^T accumulators:
+//     lane half h holds keys 4h + (r&3) + 8(r>>2) of each 32-key tile (the 32x32 C layout), so
+//     the MFMA's k slots are permuted the same way for both operands; V is quantised per
+//     (d, 64-key tile) into a transposed [d][keys] LDS image read 4 keys at a time.
+// One workgroup (8 waves) per (b, h); each wave takes 32-query tiles.  Softmax statistics, the
+// row sum and the output scaling stay f32; o is written bf16, lse f32 (natural log).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int e8m0_exp(float amax) {
+  // smallest e with amax <= 448 * 2^e (448 = 1.75 * 2^8), clamped to the E8M0 range
+  const uint32_t bits = __float_as_uint(amax);
+  const int E = (int)((bits >> 23) & 255) - 127;
+  if (((bits >> 23) & 255) == 0) return -127;  // 0 / denormal
+  const int e = (bits & 0x7fffff) <= 0x600000 ? E - 8 : E - 7;
+  return e < -127 ? -127 : (e > 127 ? 127 : e);
+}
+__device__ __forceinline__ float inv_exp2i(int e) {  // 2^-e, exact for e in [-127, 126]
+  return e >= 127 ? 0.f : __uint_as_float((uint32_t)(e == -127 ? 254 : 127 - e) << 23);
+}
+// 4 floats -> 4 e4m3 bytes (round to nearest even; |x| <= 448 by construction)
+__device__ __forceinline__ int pack_fp8x4(float a, float b, float c, float d) {
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  return __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+}
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int F8_THREADS = 512, F8_WAVES = 8;
+__device__ __forceinline__ int f8_koff(int key, int c) { return key * 64 + ((c ^ ((key >> 2) & 1)) << 4); }
+
+template <typename T> __device__ __forceinline__ void load8f(const T* p, float* x);
+template <> __device__ __forceinline__ void load8f<bf16>(const bf16* p, float* x) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int u = 0; u < 8; ++u) x[u] = (float)v[u];
+}
+template <> __device__ __forceinline__ void load8f<float>(const float* p, float* x) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p), b = *reinterpret_cast<const f32x4*>(p + 4);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) { x[u] = a[u]; x[4 + u] = b[u]; }
+}
+
+template <int NKT, typename T>  // 64-key tiles: keys padded to NKT * 64; T = the qkv / o dtype
+__global__ __launch_bounds__(F8_THREADS, 2) void attn_fwd_fp8(const T* __restrict__ qkv, int64_t ld_qkv, int D,
+                                                             int H, int N, float scale, T* __restrict__ o,
+                                                             int64_t ld_o, float* __restrict__ lse, int causal) {
+  constexpr int KEYS = NKT * 64, VROW = KEYS + 4;  // V^T rows padded: conflict-free transposed writes
+  __shared__ __attribute__((aligned(16))) unsigned char Kimg[KEYS * 64];
+  __shared__ __attribute__((aligned(16))) unsigned char Vt[64 * VROW];
+  __shared__ unsigned char Ksc[KEYS * 2];
+  __shared__ unsigned char Vsc[64 * NKT];
+  const int bh = blockIdx.x, b = bh / H, hh = bh - b * H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const T* base = qkv + (int64_t)b * N * ld_qkv + hh * 64;
+
+  // K: two adjacent lanes per key (one 32-wide d half each), one scale per key row
+  for (int t = threadIdx.x; t < KEYS * 2; t += F8_THREADS) {
+    const int key = t >> 1, half = t & 1;
+    float x[32];
+    if (key < N) {
+      const T* src = base + (int64_t)key * ld_qkv + D + half * 32;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) load8f<T>(src + c * 8, x + c * 8);
+    } else {
+#pragma unroll
+      for (int u = 0; u < 32; ++u) x[u] = 0.f;
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int u = 0; u < 32; ++u) amax = fmaxf(amax, fabsf(x[u]));
+    amax = fmaxf(amax, __shfl_xor(amax, 1, 64));  // the row's other half (KEYS * 2 is a multiple of 64)
+    const int e = e8m0_exp(amax);
+    const float inv = inv_exp2i(e);
+    int w[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) w[u] = pack_fp8x4(x[4 * u] * inv, x[4 * u + 1] * inv, x[4 * u + 2] * inv, x[4 * u + 3] * inv);
+    typedef int i32x4_ __attribute__((ext_vector_type(4)));
+    *reinterpret_cast<i32x4_*>(Kimg + f8_koff(key, 2 * half)) = i32x4_{w[0], w[1], w[2], w[3]};
+    *reinterpret_cast<i32x4_*>(Kimg + f8_koff(key, 2 * half + 1)) = i32x4_{w[4], w[5], w[6], w[7]};
+    Ksc[key * 2 + half] = (unsigned char)(e + 127);
+  }
+  // V: wave per 64-key tile, lane = d
+  for (int kt = wave; kt < NKT; kt += F8_WAVES) {
+    float x[64];
+    const T* src = base + 2 * D + lane;
+#pragma unroll
+    for (int u = 0; u < 64; ++u) {
+      const int key = kt * 64 + u;
+      x[u] = key < N ? (float)src[(int64_t)key * ld_qkv] : 0.f;
+    }
+    float amax = 0.f;
+#pragma unroll
+    for (int u = 0; u < 64; ++u) amax = fmaxf(amax, fabsf(x[u]));
+    const int e = e8m0_exp(amax);
+    const float inv = inv_exp2i(e);
+#pragma unroll
+    for (int u = 0; u < 16; ++u)
+      *reinterpret_cast<int*>(Vt + lane * VROW + kt * 64 + 4 * u) =
+          pack_fp8x4(x[4 * u] * inv, x[4 * u + 1] * inv, x[4 * u + 2] * inv, x[4 * u + 3] * inv);
+    Vsc[lane * NKT + kt] = (unsigned char)(e + 127);
+  }
+  __syncthreads();
+
+  const float c2 = scale * LOG2E;
+  const int h = lane >> 5, l31 = lane & 31;
+  const int nqt = (N + 31) / 32;
+  for (int qt = wave; qt < nqt; qt += F8_WAVES) {
+    const int q = qt * 32 + l31;
+    // Q^T fragment: this lane's 32 d values (block h) of query q
+    i32x8 qf;
+    int qsc;
+    {
+      const T* src = base + (int64_t)min(q, N - 1) * ld_qkv + h * 32;
+      float x[32];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) load8f<T>(src + c * 8, x + c * 8);
+      float amax = 0.f;
+#pragma unroll
+      for (int u = 0; u < 32; ++u) amax = fmaxf(amax, fabsf(x[u]));
+      amax = fmaxf(amax, __shfl_xor(amax, 32, 64));  // the query's other lane half: one scale per row
+      const int e = e8m0_exp(amax);
+      const float inv = inv_exp2i(e);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) qf[u] = pack_fp8x4(x[4 * u] * inv, x[4 * u + 1] * inv, x[4 * u + 2] * inv, x[4 * u + 3] * inv);
+      qsc = e + 127;
+    }
+    // online softmax over 64-key tiles (two S^T MFMAs each): only one tile's scores are live
+    float m = -INFINITY, l = 0.f;
+    f32x16 oacc[2] = {};
+#pragma unroll 1
+    for (int kt = 0; kt < NKT; ++kt) {
+      f32x16 s[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int key = (2 * kt + u) * 32 + l31;
+        typedef int i32x4_ __attribute__((ext_vector_type(4)));
+        const i32x4_ lo = *reinterpret_cast<const i32x4_*>(Kimg + f8_koff(key, 2 * h));
+        const i32x4_ hi = *reinterpret_cast<const i32x4_*>(Kimg + f8_koff(key, 2 * h + 1));
+        const i32x8 kf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        f32x16 z = {};
+        s[u] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(kf, qf, z, 0, 0, 0, Ksc[key * 2 + h], 0, qsc);
+      }
+      // rows of s[u]: key (2kt+u)*32 + 4h + (r&3) + 8(r>>2); column: query q
+      float mt = -INFINITY;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = (2 * kt + u) * 32 + 4 * h + (r & 3) + 8 * (r >> 2);
+          if (key >= N || (causal && key > q)) s[u][r] = -INFINITY;
+          mt = fmaxf(mt, s[u][r]);
+        }
+      mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+      const float mn = fmaxf(m, mt);  // finite from the first tile on: key 0 is never masked
+      const float alpha = fexp2((m - mn) * c2);  // first tile: m = -inf -> 0
+      m = mn;
+      const float mc = m * c2;
+      l *= alpha;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) oacc[dt] *= alpha;
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float p = fexp2(fmaf(s[u][r], c2, -mc));
+          s[u][r] = p;
+          l += p;
+        }
+      i32x8 pf;  // P^T fragment: byte j = tile (j/16), register j%16, times 2^8
+#pragma unroll
+      for (int w = 0; w < 8; ++w) {
+        const f32x16& t = s[w >> 2];
+        const int r = 4 * (w & 3);
+        pf[w] = pack_fp8x4(t[r] * 256.f, t[r + 1] * 256.f, t[r + 2] * 256.f, t[r + 3] * 256.f);
+      }
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt) {
+        const int d = dt * 32 + l31;
+        const unsigned char* row = Vt + d * VROW + kt * 64 + 4 * h;
+        i32x8 vf;
+#pragma unroll
+        for (int w = 0; w < 8; ++w) vf[w] = *reinterpret_cast<const int*>(row + (w >> 2) * 32 + 8 * (w & 3));
+        oacc[dt] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(vf, pf, oacc[dt], 0, 0, 0, Vsc[d * NKT + kt], 0,
+                                                                   127 - 8);
+      }
+    }
+    l += __shfl_xor(l, 32, 64);
+    const float mc = m * c2;
+    if (q < N) {
+      const float inv = 1.0f / l;
+      T* orow = o + ((int64_t)b * N + q) * ld_o + hh * 64;
+#pragma unroll
+      for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int mq = 0; mq < 4; ++mq) {
+          const int d = dt * 32 + 4 * h + 8 * mq;
+          const f32x4 ov = {oacc[dt][4 * mq] * inv, oacc[dt][4 * mq + 1] * inv, oacc[dt][4 * mq + 2] * inv,
+                            oacc[dt][4 * mq + 3] * inv};
+          if constexpr (sizeof(T) == 2) *reinterpret_cast<bf16x4*>(orow + d) = bf16x4{(bf16)ov[0], (bf16)ov[1], (bf16)ov[2], (bf16)ov[3]};
+          else *reinterpret_cast<f32x4*>(orow + d) = ov;
+        }
+      if (h == 0 && lse) lse[(int64_t)bh * N + q] = (mc + __log2f(l)) * LN2;
+    }
+  }
+}
+
 // qkv-bias gradient partials of one (b, h): sum this workgroup's rows of dq (or dk, dv)
 // -- per lane over its rows, across the 16 lanes of a row group, across the 8 waves
 // through LDS (reused after the main loop) -- into out[0..63] (and out[D..] for dk,
@@ -682,6 +901,30 @@ int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
     hipLaunchKernelGGL(attn_fwd_generic<bf16>, grid, dim3(256), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale, (bf16*)o, ld_o, lse, causal);
   else
     hipLaunchKernelGGL(attn_fwd_generic<float>, grid, dim3(256), 0, s, (const float*)qkv, ld_qkv, D, H, N, scale, (float*)o, ld_o, lse, causal);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+// fp8 (block-scaled OCP e4m3) forward, head_dim 64, N <= 320: see attn_fwd_fp8.  qkv / o bf16
+// or f32 (dtype; quantised to e4m3 inside the kernel either way); lse f32 or null.
+int vit_sdpa_fwd_fp8(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, void* o,
+                     int64_t ld_o, float* lse, float scale, int causal, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (head_dim != 64 || N <= 0 || N > 320 || (ld_qkv % 8) || (ld_o % 4)) return (int)hipErrorInvalidValue;
+  const int D = H * 64;
+  switch ((N + 63) / 64) {
+#define F8(n)                                                                                                   \
+  case n:                                                                                                       \
+    if (dtype == VIT_BF16)                                                                                      \
+      hipLaunchKernelGGL((attn_fwd_fp8<n, bf16>), dim3(B * H), dim3(F8_THREADS), 0, s, (const bf16*)qkv, ld_qkv, \
+                         D, H, N, scale, (bf16*)o, ld_o, lse, causal);                                          \
+    else                                                                                                        \
+      hipLaunchKernelGGL((attn_fwd_fp8<n, float>), dim3(B * H), dim3(F8_THREADS), 0, s, (const float*)qkv,      \
+                         ld_qkv, D, H, N, scale, (float*)o, ld_o, lse, causal);                                 \
+    break;
+    F8(1) F8(2) F8(3) F8(4) F8(5)
+#undef F8
+  }
   VIT_CHECK_LAUNCH();
   return 0;
 }

@@ -251,6 +251,7 @@ class CLIP(nn.Module):
         self.logit_scale = nn.Parameter(torch.ones([]) * math.log(1 / 0.07))
         self._shadows = None
         self._text_cache = None
+        self.attention_fp8 = False  # set_attention_fp8
         self.initialize_parameters()
 
     @torch.no_grad()
@@ -293,8 +294,16 @@ class CLIP(nn.Module):
                 self._shadows.add(p, T)
         self._shadows.refresh()
 
-    def _cfg(self, heads, causal):
-        return dict(heads=heads, eps=1e-5, quick_gelu=True, dtype=self.compute_dtype, causal=causal)
+    def set_attention_fp8(self, enable: bool = True):
+        """Block-scaled e4m3 attention (vit_sdpa_fwd_fp8, BASELINE configs[4]) in every block whose
+        forward needs no backward: the frozen blocks in front of the first trainable one in each
+        tower (CLIP-HBA trains only the DoRA blocks 22-23 / 11, NEWP:484-544) and all blocks of a
+        no-grad pass (evaluation, behavioural RSA).  Trainable blocks keep bf16/f32 attention."""
+        self.attention_fp8 = bool(enable)
+
+    def _cfg(self, heads, causal, frozen=False):
+        fp8 = self.attention_fp8 and (frozen or not torch.is_grad_enabled())
+        return dict(heads=heads, eps=1e-5, quick_gelu=True, dtype=self.compute_dtype, causal=causal, attn_fp8=fp8)
 
     # -- towers -----------------------------------------------------------------
     def encode_image(self, image, pos_embedding=True):
@@ -320,8 +329,10 @@ class CLIP(nn.Module):
                                       v.ln_pre.bias.detach(), 1e-5, torch.float32, need_stats=False)
         x = x2.reshape(B, npatch + 1, W)
         heads = W // 64
-        for blk in v.transformer.resblocks:
-            x = _BlockFn.apply(x, *blk.block_params(), self._cfg(heads, False))
+        blocks = list(v.transformer.resblocks)
+        first = _first_trainable(blocks)
+        for i, blk in enumerate(blocks):
+            x = _BlockFn.apply(x, *blk.block_params(), self._cfg(heads, False, frozen=i < first))
         idx = self._cls_rows(B, npatch + 1, x.device)
         return _PoolHeadFn.apply(x, idx, v.ln_post.weight, v.ln_post.bias, v.proj, 1e-5)
 
@@ -343,7 +354,7 @@ class CLIP(nn.Module):
             raise NotImplementedError("gradients into the CLIP token/positional embedding are not on the "
                                       "CLIP-HBA path (switch_dora_layers freezes them, NEWP:516-544)")
         params = emb + [p for b in blocks[:k] for p in b.parameters()]
-        key = (text.data_ptr(), text._version, tuple(text.shape), k, self.compute_dtype,
+        key = (text.data_ptr(), text._version, tuple(text.shape), k, self.compute_dtype, self.attention_fp8,
                tuple((p.data_ptr(), p._version) for p in params))
         if self.cache_frozen_text and self._text_cache is not None and self._text_cache[0] == key:
             return self._text_cache[1], k
@@ -352,7 +363,7 @@ class CLIP(nn.Module):
         x = x.reshape(S, Lq, -1)
         with torch.no_grad():
             for blk in blocks[:k]:
-                x = _BlockFn.apply(x, *blk.block_params(), self._cfg(blk.attn.num_heads, True))
+                x = _BlockFn.apply(x, *blk.block_params(), self._cfg(blk.attn.num_heads, True, frozen=True))
         if self.cache_frozen_text:
             self._text_cache = (key, x)
         return x, k
@@ -426,7 +437,7 @@ class CLIPHBA(nn.Module):
     ``backbone_name`` and :func:`tokenize` ids are used (no network)."""
 
     def __init__(self, classnames, backbone_name="ViT-L/14", pos_embedding=False, clip_model=None,
-                 tokenized_prompts=None, compute_dtype=torch.float32):
+                 tokenized_prompts=None, compute_dtype=torch.float32, attention_fp8=False):
         super().__init__()
         self.num_clip = len(classnames)
         if clip_model is None:
@@ -436,6 +447,8 @@ class CLIPHBA(nn.Module):
             clip_model = CLIP(compute_dtype=compute_dtype, **_BACKBONES[backbone_name])
         self.clip_model = clip_model
         self.clip_model.float()
+        if attention_fp8:  # BASELINE configs[4]: fp8 attention in the frozen / no-grad blocks
+            self.clip_model.set_attention_fp8(True)
         self.pos_embedding = pos_embedding
         for p in self.clip_model.parameters():
             p.requires_grad = False

@@ -271,6 +271,7 @@ class _BlockFn(torch.autograd.Function):
         dact, act = torch.empty(M, F, dtype=T, device=dev), torch.empty(M, F, dtype=T, device=dev)
         Wqkv, Wproj, W1, W2 = _wt(qkvw, T), _wt(projw, T), _wt(fc1w, T), _wt(fc2w, T)
         causal = bool(cfg.get("causal", False))
+        attn_fp8 = bool(cfg.get("attn_fp8", False))  # forward-only blocks (frozen prefix, no-grad passes)
 
         def chain(b0, b1):
             """The block over images [b0, b1) (rows b0*N .. b1*N of every tensor) as its 7 launches."""
@@ -280,7 +281,8 @@ class _BlockFn(torch.autograd.Function):
                 lambda: ops.layer_norm_fwd(x2[sl], n1w.detach(), n1b.detach(), eps, T, out=h1[sl], mean=m1[sl],
                                            rstd=r1[sl]),
                 lambda: ops.linear_fwd(h1[sl], Wqkv, qkvb.detach(), out=qkv[sl]),
-                lambda: ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N], causal=causal),
+                lambda: ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N], causal=causal,
+                                     fp8=attn_fp8),
                 lambda: ops.linear_fwd(o[sl], Wproj, projb.detach(), epi=L.EPI_RESID, resid=x2[sl], out=xm[sl]),
                 lambda: ops.layer_norm_fwd(xm[sl], n2w.detach(), n2b.detach(), eps, T, out=h2[sl], mean=m2[sl],
                                            rstd=r2[sl]),
@@ -317,6 +319,7 @@ class _BlockFn(torch.autograd.Function):
         ctx.wops = (Wqkv, Wproj, W1, W2)
         ctx.meta = (B, N, D, H, T, cfg.get("compact_np", 0), cfg["quick_gelu"], causal)
         ctx.defer_bwd = bool(cfg.get("defer_bwd_join"))
+        ctx.attn_fp8 = attn_fp8
         ctx.grad_hook = cfg.get("grad_hook")
         ctx.flat_span = cfg.get("flat_span")
         return xo.reshape(B, N, D)
@@ -337,6 +340,9 @@ class _BlockFn(torch.autograd.Function):
         need_mlp_in = any(ng[0:11])     # anything upstream of fc2 (its input gradient path)
         need_attn = any(ng[0:5])        # anything upstream of proj
         need_h1 = any(ng[0:3])
+        if need_attn and ctx.attn_fp8:
+            raise RuntimeError("this block's attention ran in fp8 (forward only); its backward needs the bf16 "
+                               "forward: enable fp8 attention only for frozen blocks / no-grad passes")
         # gradient buffers are taken on the main stream (allocator ownership), filled on the side stream
         g = [None] * 13
         dpre = dxm = dxm_c = do = dqkv = None
@@ -523,6 +529,7 @@ class VisionTransformer(nn.Module):
         self.head = nn.Linear(embed_dim, num_classes)
         self._shadows = None
         self._defer_grad_join = False
+        self._attn_fp8 = False
         self.init_weights()
 
     # timm init_weights_vit_timm; exact RNG stream differs from timm
@@ -597,6 +604,12 @@ class VisionTransformer(nn.Module):
         with gradient hooks, which read ``.grad`` during the backward on the caller's stream."""
         self._defer_grad_join = bool(enable)
 
+    def set_attention_fp8(self, enable: bool = True):
+        """Run attention as block-scaled e4m3 MFMA (vit_sdpa_fwd_fp8) in forward passes that build no
+        autograd graph (``torch.no_grad()``: validation, ``compute_rsa_score``'s embeddings) --
+        BASELINE configs[4].  Training forwards keep the bf16 kernels their backward needs."""
+        self._attn_fp8 = bool(enable)
+
     def set_grad_ready_hook(self, fn):
         """fn(lo, hi) is called by each block's backward once the block's gradients (the flat
         buffer's [lo, hi)) are enqueued, on the stream they were enqueued on
@@ -629,6 +642,8 @@ class VisionTransformer(nn.Module):
                                  and torch.is_grad_enabled() and pe.proj.weight.requires_grad
                                  and all(p.grad is None for p in self.parameters()))
         hook = getattr(self, "_grad_hook", None) if cfg["defer_bwd_join"] else None
+        # fp8 attention (set_attention_fp8): forward passes that build no graph (eval / RSA)
+        cfg["attn_fp8"] = self._attn_fp8 and not torch.is_grad_enabled()
         for i, blk in enumerate(self.blocks):
             bcfg = cfg if i != 0 else dict(cfg, compact_np=pe.num_patches)
             if hook is not None:

@@ -234,14 +234,17 @@ def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0
 # attention
 # ----------------------------------------------------------------------------
 
-def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None, lse=None, causal=False):
+def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None, lse=None, causal=False, fp8=False):
+    """softmax(q k^T * scale) v per (b, h) from the fused qkv [B*N, 3D]; fp8: the block-scaled e4m3
+    MFMA kernel (forward only: its lse is not the bf16 backward's)."""
     D = H * 64
     if o is None:
         o = torch.empty(B * N, D, dtype=qkv2d.dtype, device=qkv2d.device)
     if lse is None:
         lse = torch.empty(B * H * N, dtype=torch.float32, device=qkv2d.device)
     scale = 64 ** -0.5 if scale is None else scale
-    call("vit_sdpa_fwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(lse),
+    name = "vit_sdpa_fwd_fp8" if fp8 else "vit_sdpa_fwd"
+    call(name, L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(lse),
          float(scale), int(causal), _s(qkv2d))
     return o, lse
 
