@@ -256,3 +256,52 @@ def test_sweep_condition_on_cliphba(tmp_path):
     with open(done[0][1]) as fh:
         out = fh.read().splitlines()
     assert out[0].split(",") == S.CSV_HEADERS and out[1].split(",")[0] == "2" and out[1].split(",")[6] == "True"
+
+
+def _make_fp8_cliphba():
+    """CLIPHBA(ViT-L/14) + DoRA with fp8 attention in the frozen blocks (BASELINE configs[4]) and its
+    AdamW -- module level so the sweep launcher's worker processes can rebuild it."""
+    import vit_amd
+    torch.manual_seed(0)
+    m = vit_amd.CLIPHBA(["c%d" % i for i in range(66)], "ViT-L/14", pos_embedding=True, attention_fp8=True)
+    vit_amd.apply_dora_to_ViT(m, n_vision_layers=2, n_transformer_layers=1, r=32)
+    vit_amd.switch_dora_layers(m, freeze_all=True, dora_state=True)
+    m = m.cuda()
+    return m, vit_amd.FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=3e-4)
+
+
+@pytest.mark.gpu
+def test_c5_sweep_launcher_fp8_on_cliphba(tmp_path):
+    """Config C5 end to end at small scale: a baseline run, then the process-per-GPU sweep launcher
+    (two worker processes sharing this box's one GPU) over a start x length grid on the real
+    CLIPHBA with fp8 attention; every condition once, longer windows resumed from their siblings."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import numpy as np
+    import vit_amd
+    from vit_amd import sweep as S
+    g = torch.Generator().manual_seed(1)
+    mk = lambda n: (torch.randn(n, 3, 224, 224, generator=g), torch.randn(n, 66, generator=g) + 2)
+    a = np.random.default_rng(0).random((48, 48))
+    ref = (a + a.T) / 2
+    np.fill_diagonal(ref, 0)
+    data = dict(train=mk(16), test=mk(8), inference=torch.randn(48, 3, 224, 224, generator=g), reference_rdm=ref)
+    m, opt = _make_fp8_cliphba()
+    dev = {k: (tuple(t.cuda() for t in v) if isinstance(v, tuple) else (v.cuda() if torch.is_tensor(v) else v))
+           for k, v in data.items()}
+    base = tmp_path / "base"
+    S.train_condition(m, opt, vit_amd.mse_loss, dev, epochs=2, training_run=1, perturb_length=0, perturb_type=None,
+                      batch_size=8, training_res_path=str(tmp_path / "b.csv"), dora_parameters_path=str(base / "dora"),
+                      random_state_path=str(base / "rs"), dataloader_generator=torch.Generator().manual_seed(0))
+    del m, opt, dev
+    conds = [(2, 1), (2, 2), (3, 1)]
+    res = S.launch_sweep(2, _make_fp8_cliphba, vit_amd.mse_loss, data, conds, gpus=[0], perturb_type="random_target",
+                         out_dir=str(tmp_path / "sw"), baseline_dora_path=str(base / "dora"),
+                         baseline_random_state_path=str(base / "rs"), epochs=4, batch_size=8, torch_threads=4)
+    flat = {c: (p, src) for r in res.values() for c, p, src in r}
+    assert sorted(flat) == sorted(conds)
+    assert flat[(2, 2)][1] == "sibling l1" and flat[(2, 1)][1] == "baseline"
+    for (e, l), (path, _) in flat.items():
+        with open(path) as fh:
+            rows = [r.split(",") for r in fh.read().splitlines()[1:]]
+        assert [int(r[0]) for r in rows] == list(range(e, 5)) and all(np.isfinite(float(r[2])) for r in rows)

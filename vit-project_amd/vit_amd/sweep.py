@@ -350,7 +350,10 @@ def _sweep_worker(rank, world, make_model_and_optimizer, criterion, data, condit
     if threads:
         torch.set_num_threads(threads)
     if devices:
-        torch.cuda.set_device(devices[rank % len(devices)])
+        dev = torch.device("cuda", devices[rank % len(devices)])
+        torch.cuda.set_device(dev)
+        mv = lambda t: t.to(dev) if torch.is_tensor(t) else t
+        data = {k: (tuple(mv(t) for t in v) if isinstance(v, tuple) else mv(v)) for k, v in data.items()}
     out = run_sweep(make_model_and_optimizer, criterion, data, conditions, rank=rank, world=world, **kw)
     results.put((rank, out))
 
