@@ -37,7 +37,7 @@ struct Epi {
   int n_patch;              // EPI_PATCH: patches per image (seq = n_patch + 1)
   int64_t slab;             // split-r: element offset of slab z
   float* csum;              // optional column sums of the epilogue output: [ceil(M/64)][N] partials (64-row groups)
-  int dbg;                  // timing experiments only (vit_gemm_variant(v + 100*bits)): 1 = no in-loop loads, 2 = no in-loop barriers, 4 = no epilogue
+  int dbg;                  // timing experiments only (vit_gemm_variant(v + 100*bits)): 1 = no in-loop loads, 2 = no in-loop barriers, 4 = no epilogue, 16 = fragment epilogue
 };
 
 template <typename T> __device__ __forceinline__ void store4(T* p, f32x4 v);
@@ -240,8 +240,9 @@ template <class C, typename TO> struct EpiLds {
 // dwordx4 store instead of two dwordx2 (the fragment-layout store tail is issue-bound).
 // Needs N % 32 == 0 (whole 8-column groups).
 template <int EPI, typename TO, typename TA>
-__device__ __forceinline__ f32x4 epi_val(const Epi& e, int i, int j, f32x4 v, bool ok, f32x4& o0, f32x4& o1) {
-  if (e.bias && ok) v += *reinterpret_cast<const f32x4*>(e.bias + j);
+__device__ __forceinline__ f32x4 epi_val(const Epi& e, int i, int j, f32x4 v, bool ok, f32x4& o0, f32x4& o1,
+                                         const f32x4& bias4) {
+  v += bias4;  // this lane's 4 bias values (zero without bias), loaded once per column fragment
   if constexpr (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) {
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -280,9 +281,13 @@ __device__ __forceinline__ void epilogue_swap(const Epi& e, const f32x4 (&acc)[C
   constexpr bool two = EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU;
   const int g = lane >> 4;
   const int colsel = (g & 1) * 16 + (g >> 1) * 8;
-  f32x4 cs[C::AJ];
+  f32x4 cs[C::AJ], bias4[C::AJ];
 #pragma unroll
-  for (int b = 0; b < C::AJ; ++b) cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int b = 0; b < C::AJ; ++b) {
+    cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int j = j0 + wj * C::WN + b * 16 + 4 * g;
+    bias4[b] = (e.bias && j < N) ? *reinterpret_cast<const f32x4*>(e.bias + j) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int a = 0; a < C::AI; ++a) {
     const int i = i0 + wi * C::WM + a * 16 + (lane & 15);
@@ -293,8 +298,8 @@ __device__ __forceinline__ void epilogue_swap(const Epi& e, const f32x4 (&acc)[C
       const int ja = jp + 4 * g, jb = jp + 16 + 4 * g;
       const bool oka = row_ok && ja < N, okb = row_ok && jb < N;
       f32x4 xa, ya, xb, yb;
-      const f32x4 va = epi_val<EPI, TO, TA>(e, i, ja, acc[a][b], oka, xa, ya);
-      const f32x4 vb = epi_val<EPI, TO, TA>(e, i, jb, acc[a][b + 1], okb, xb, yb);
+      const f32x4 va = epi_val<EPI, TO, TA>(e, i, ja, acc[a][b], oka, xa, ya, bias4[b]);
+      const f32x4 vb = epi_val<EPI, TO, TA>(e, i, jb, acc[a][b + 1], okb, xb, yb, bias4[b + 1]);
       if (e.csum) {
         if (oka) cs[b] += va;
         if (okb) cs[b + 1] += vb;
@@ -553,19 +558,16 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// One output tile (unit w of the 1-D (split, tile) space) of the fast bf16 GEMM.
 template <class C, int PL, int QL, int EPI, typename TO, typename TA>
-__global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __restrict__ P, int64_t ldp,
-                                                                  const bf16* __restrict__ Q, int64_t ldq,
-                                                                  int M, int N, int R, int r_chunk, Epi e) {
+__device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ldp, const bf16* __restrict__ Q,
+                                          int64_t ldq, int M, int N, int R, int r_chunk, const Epi& e, int w,
+                                          char* smem) {
   constexpr int S = C::STAGES, BM = C::BM, BN = C::BN, BK = C::BK;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // 1-D grid over (split, tile): consecutive ids share an XCD after the remap,
-  // so a split's workgroups (same rows of P and Q) sit on one L2
   const int tiles_j = (N + BN - 1) / BN;
   const int tiles = ((M + BM - 1) / BM) * tiles_j;
-  const int w = xcd_remap(blockIdx.x, gridDim.x);
   const int z = w / tiles, t = w - z * tiles;
   const int ti = t / tiles_j, tj = t - ti * tiles_j;
   const int i0 = ti * BM, j0 = tj * BN;
@@ -661,11 +663,20 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
   // 256x256 tile and the GELU / GELU' epilogues are faster through the row-contiguous LDS
   // staging (tools/bench_kernels.py --sweep: v vs 6400 + v).  Timing flags: dbg 64 forces the
   // staged epilogue, dbg 8 the plain fragment-layout one below (8-B stores).
-  if constexpr (sizeof(TO) == 2 && ((EPI == EPI_STORE && C::BM * C::BN < 256 * 256) ||
+  // (plain bf16 stores: fragment epilogue on every tile -- the qkv forward on the 256x256 tile runs 10 %
+  // faster than through the LDS staging, tools/bench_kernels.py --sweep=5,1605; the GELU pair stays staged)
+  if constexpr (sizeof(TO) == 2 && (EPI == EPI_STORE ||
                                      (C::EPS == 1 && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU ||
                                                       EPI == EPI_BIAS_QGELU || EPI == EPI_GELU_BWD ||
                                                       EPI == EPI_QGELU_BWD)))) {
     if (!(e.dbg & (8 | 64)) && N % 32 == 0) {
+      epilogue_swap<C, EPI, TO, TA>(e, acc, i0, j0, wi, wj, lane, M, N);
+      return;
+    }
+  }
+  if constexpr (sizeof(TO) == 2 && C::EPS == 0 && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU ||
+                                                    EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD)) {
+    if ((e.dbg & 16) && N % 32 == 0) {  // timing experiment: the fragment (permlane16) epilogue on any tile
       epilogue_swap<C, EPI, TO, TA>(e, acc, i0, j0, wi, wj, lane, M, N);
       return;
     }
@@ -693,6 +704,16 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
     }
     if (e.csum && (a & 3) == 3) csum_flush<C::AJ>(e, cs, i0 + wi * C::WM + (a - 3) * 16, M, N, j0 + wj * C::WN, lane);
   }
+}
+
+// 1-D grid over (split, tile): consecutive ids share an XCD after the remap, so a split's
+// workgroups (same rows of P and Q) sit on one L2
+template <class C, int PL, int QL, int EPI, typename TO, typename TA>
+__global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __restrict__ P, int64_t ldp,
+                                                                  const bf16* __restrict__ Q, int64_t ldq,
+                                                                  int M, int N, int R, int r_chunk, Epi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  gemm_tile<C, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, r_chunk, e, xcd_remap(blockIdx.x, gridDim.x), smem);
 }
 
 // ----------------------------------------------------------------------------
