@@ -19,6 +19,7 @@
 // odd shapes (classifier head N=1000).
 #include "common.hpp"
 #include "reduce.hpp"
+#include <stdlib.h>
 #include <string.h>
 #include <type_traits>
 
@@ -898,7 +899,9 @@ __global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, 
 
 // the configurations kept after the sweep (tools/bench_kernels.py --sweep; DESIGN.md
 // lists the measured TFLOP/s per shape).  Others tried: 256x256x32 S5 with register
-// double-buffering (1 WG/CU; wgrad 360-400 TF), 128x128x32 S4, 256x128x64 S3, 128x256x32 S4.
+// double-buffering (1 WG/CU; wgrad 360-400 TF), 128x128x32 S4, 256x128x64 S3, 128x256x32 S4,
+// 256x256x32 S3 / S4 (V5's waves, deeper ring: qkv forward +6 % standalone, the other shapes flat
+// or slower; as the in-step weight gradient -0.4 .. -0.7 % step rate vs the ping-pong kernel).
 //            BM   BN  BK WI WJ  S  DB    OCC
 using V1 = Cfg<256, 128, 32, 4, 2, 3, false, 4>;  //  72 KiB, 2 WG/CU: dgrad
 using V2 = Cfg<128, 128, 64, 2, 2, 2, false, 2>;  //  64 KiB, 2 WG/CU (4 waves): N = 768 forward
@@ -1053,12 +1056,23 @@ static bool any_fast_ok(int dtype, int pl, int ql, int M, int N, int R, const vo
 static int g_variant = -1;  // -1: per-shape choice; 1, 2, 5: force big::V<n>, 8, 9: ping-pong (tuning)
 static int g_dbg = 0;
 
+// per-class override for in-step A/B runs (tools/ab_bench.sh): VIT_GEMM_{FWD,DGRAD,WGRAD}=<variant>
+static int env_variant(const char* name) {
+  const char* s = getenv(name);
+  return s && *s ? atoi(s) : -1;
+}
+
 // per-shape choice among the kept configurations (sweep on MI355X, bs=256 ViT-B/16 shapes)
 static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool pers_ok, bool act_bwd) {
+  static const int o_fwd = env_variant("VIT_GEMM_FWD"), o_dgrad = env_variant("VIT_GEMM_DGRAD"),
+                   o_wgrad = env_variant("VIT_GEMM_WGRAD");
+  const bool wgrad = split > 1 || (pl == LAY_CR && ql == LAY_CR), fwd = pl == LAY_RC && ql == LAY_RC;
+  const int o = wgrad ? o_wgrad : fwd ? o_fwd : o_dgrad;
   int v;
   if (g_variant >= 0) v = g_variant % 100;
-  else if (split > 1 || (pl == LAY_CR && ql == LAY_CR)) v = 8;           // wgrad: ping-pong 256x256
-  else if (pl == LAY_RC && ql == LAY_RC) v = (N >= 1536 || R >= 1536) ? 5 : 2;  // forward
+  else if (o >= 0) v = o;
+  else if (wgrad) v = 8;                                                   // wgrad: ping-pong 256x256
+  else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : 2;                     // forward
   else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;                // dgrad (GELU' epilogue: V1, 2 WG/CU)
   (void)M;
   if ((v == 2 || v == 5 || v == 10) && R % 64) v = 1;                       // BK = 64 configurations need 64-row chunks
