@@ -6,7 +6,10 @@ the data loader).  N>1: one process per GPU, 256 images per rank (weak scaling),
 gradients averaged with RCCL all-reduces issued block by block during the
 backward (DDP in the reference, VIT:287).  Prints ONE JSON line on rank 0.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--graph]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--graph] [--no-c3] [--no-cpu]
+
+At N=1 the line also carries ``c3``: the CLIP-HBA step (BASELINE configs[2]) timed in fp32, the
+reference's precision, and in the bf16 opt-in -- an extra key, not the headline value.
 
 ``--gpus N`` without a torchrun environment launches its own N ranks (one
 process per GPU, ``torch.distributed.run`` on 127.0.0.1, as the reference's
@@ -49,6 +52,7 @@ def parse(argv=None):
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-overlap", action="store_true", help="weight gradients inline instead of on a side stream")
     ap.add_argument("--no-probe", action="store_true", help="no HIP events around the weight-gradient launches")
+    ap.add_argument("--no-c3", action="store_true", help="skip the CLIP-HBA (config C3) leg")
     ap.add_argument("--dry", action="store_true", help="CPU/gloo launcher + gradient-averaging check, no GPU")
     return ap.parse_args(argv)
 
@@ -144,6 +148,78 @@ def _pmc_traffic(name):
         except (OSError, KeyError, ValueError):
             continue
     return None, None
+
+
+# ----------------------------------------------------------------------------
+# config C3 leg: CLIP-HBA ViT-L/14 + DoRA train step, in both dtypes
+# ----------------------------------------------------------------------------
+
+PEAK_F32_TFLOPS = 256 * 4 * 64 * 2.4e9 / 1e12  # v_mfma_f32_16x16x4_f32: 64 FLOP/clk/SIMD
+
+
+def _block_flops(tokens, width, seq):
+    """forward FLOPs of one pre-LN transformer block (qkv, attention, out_proj, MLP 4x)."""
+    return 2 * tokens * width * (3 * width + width + 8 * width) + 4 * tokens * seq * width
+
+
+def c3_step_flop(batch):
+    """Analytic FLOPs of one C3 step: the visual tower forward (24 blocks + patch embedding), the
+    last text block forward (66 prompts x 77 tokens; blocks 0-10 are a cached frozen prefix), and
+    the backward through the two DoRA visual blocks and the DoRA text block (input gradients 2x,
+    DoRA weight gradients 1x their forward GEMM FLOPs)."""
+    vis = _block_flops(batch * 257, 1024, 257)
+    txt = _block_flops(66 * 77, 768, 77)
+    fwd = 24 * vis + 2 * batch * 256 * 588 * 1024 + txt
+    bwd = 2 * (2 * vis) + 2 * txt
+    return fwd + bwd
+
+
+def c3_leg(dev, dtype="f32", batch=64, steps=10, warmup=3):
+    """One C3 step rate (BASELINE configs[2]): CLIPHBA ViT-L/14, DoRA r=32 on the last 2 visual
+    blocks and the last text out_proj (NEWP:484-544), MSE on 66-D targets, fused AdamW
+    (NEWP:994-1001, 1181).  Random-init weights and synthetic images (OpenAI weights and THINGS
+    images are absent offline).  f32 = the reference's precision (NEWP:274), bf16 the opt-in."""
+    import torch
+    import vit_amd
+    T = torch.float32 if dtype == "f32" else torch.bfloat16
+    torch.manual_seed(0)
+    m = vit_amd.CLIPHBA(["class%d" % i for i in range(66)], "ViT-L/14", pos_embedding=True, compute_dtype=T)
+    vit_amd.apply_dora_to_ViT(m, n_vision_layers=2, n_transformer_layers=1, r=32)
+    vit_amd.switch_dora_layers(m, freeze_all=True, dora_state=True)
+    m = m.to(dev)
+    opt = vit_amd.FusedAdamW([p for p in m.parameters() if p.requires_grad], lr=3e-4)
+    x = torch.randn(batch, 3, 224, 224, device=dev)
+    y = torch.randn(batch, 66, device=dev) * 0.5 + 1.0
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = vit_amd.mse_loss(m(x), y)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(warmup):
+        loss = step()
+    torch.cuda.synchronize(dev)
+    marks = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    t0 = time.perf_counter()
+    marks[0].record()
+    for i in range(steps):
+        loss = step()
+        marks[i + 1].record()
+    torch.cuda.synchronize(dev)
+    el = time.perf_counter() - t0
+    med = statistics.median(marks[i].elapsed_time(marks[i + 1]) for i in range(steps))
+    fl = c3_step_flop(batch)
+    tf = fl * steps / el / 1e12
+    peak = PEAK_F32_TFLOPS if dtype == "f32" else PEAK_BF16_TFLOPS
+    out = {"value": round(batch * steps / el, 2), "unit": "images/s", "ms_per_step": round(el / steps * 1e3, 3),
+           "ms_per_step_median": round(med, 3), "batch": batch, "steps": steps, "warmup": warmup, "dtype": dtype,
+           "step_tflop": round(fl / 1e12, 3), "achieved_tflops": round(tf, 1), "peak_tflops": round(peak, 1),
+           "frac_of_peak": round(tf / peak, 4), "final_loss": round(float(loss.item()), 4)}
+    del m, opt, x, y, loss
+    torch.cuda.empty_cache()
+    return out
 
 
 # ----------------------------------------------------------------------------
@@ -370,6 +446,12 @@ def main(a):
         out["per_rank_s"] = [round(v, 4) for v in per_rank]
         out["allreduce_exposed_ms_median"] = None if red_ms is None else round(red_ms, 3)
         out["allreduce"] = "overlapped per block (side stream)" if reducer is not None else "bucketed after backward"
+    if world == 1 and not a.no_c3:
+        # extra key, not the headline: BASELINE configs[2] (C3) at the reference's fp32 and the bf16 opt-in
+        out["c3"] = {"workload": "CLIP-HBA ViT-L/14 + DoRA train step (fwd+MSE+bwd+AdamW), BASELINE configs[2]",
+                     "metric": "images/sec", "data": "synthetic images [64,3,224,224] + 66-D targets; random-init "
+                                                     "weights (OpenAI weights absent offline)",
+                     "f32": c3_leg(dev, "f32"), "bf16": c3_leg(dev, "bf16")}
     if world == 1 and not a.no_cpu:
         out["cpu_baseline"] = cpu_baseline(a.cpu_seconds)
     print(json.dumps(out), flush=True)
