@@ -348,7 +348,9 @@ def _sdpa_ref(qkv, B, H, N):
     return o, lse.reshape(-1), (q, k, v)
 
 
-@pytest.mark.parametrize("N", [197, 50, 257, 16])
+# bf16 backward: one fused kernel for N <= 224 (16 .. 224 cover 1 .. 14 waves, odd and even tile
+# counts), the two-kernel form above (225, 257)
+@pytest.mark.parametrize("N", [197, 50, 257, 16, 224, 208, 33, 225])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_sdpa_fwd_bwd(N, dtype):
     B, H = 2, 3
@@ -376,7 +378,7 @@ def test_sdpa_fwd_bwd(N, dtype):
     _close(g[:, 2 * D:], dv, rel, "dv")
 
 
-@pytest.mark.parametrize("N", [77, 16, 197])
+@pytest.mark.parametrize("N", [77, 16, 197, 224])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_sdpa_causal_fwd_bwd(N, dtype):
     """Causal mask (CLIP text tower attn_mask: -inf above the diagonal) vs a torch fp32 reference."""

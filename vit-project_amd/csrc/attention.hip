@@ -482,7 +482,7 @@ __device__ __forceinline__ void bias_flush_c(const float (&own)[NOUT], char* sme
 
 // ---------------------------------------------------------------------------
 // bf16 backward, two kernels per (b, h) so each holds only half the head in LDS
-// (57 KiB -> two workgroups per CU):
+// (57 KiB -> two workgroups per CU); N > 224 (CLIP ViT-L/14's 257 tokens), else attn_bwd_fused:
 //   attn_bwd_dq  : LDS K, V; each wave owns query tiles (Q, dO, O from global),
 //                  computes delta = rowsum(dO*O) (written for the other kernel),
 //                  recomputes S^T, dP^T over all keys, accumulates dQ.
@@ -668,6 +668,224 @@ __global__ __launch_bounds__(AT_THREADS, 4) void attn_bwd_dkv(const bf16* __rest
     }
   }
   if (bias_part) bias_flush_c<2>(cs, smem, bias_part + (int64_t)b * 3 * D + h * 64, D);
+}
+
+// ---------------------------------------------------------------------------
+// bf16 backward fused into one kernel per (b, h) for N <= 224 (NT <= 14 tiles of 16): one
+// workgroup of NT waves, so each wave owns exactly one key tile in phase 1 and one query tile
+// in phase 2.  q, k, v, o, dO are read once and S, dP computed once (the two-kernel form
+// recomputes both and reads q, k, v, dO twice).
+//   prologue: Q, dO -> LDS images; delta = rowsum(dO * O) (O straight from global) and lse -> LDS;
+//             wave w holds key tile w's K, V rows in registers.
+//   phase 1 : wave w: S, dP of its 16 keys against every query (the attn_bwd_dkv loop) ->
+//             dK, dV; dS^T goes to LDS as NT column tiles [key row][16 queries] bf16, the layout
+//             the transposed read of phase 2 takes conflict-free (16 rows x 32 B per group).
+//   phase 2 : the K tiles replace the Q image; wave w: dQ of its 16 queries = dS K over all keys
+//             (A = K^T and B = dS^T from the same transposed-read pattern: same k-slot order).
+// LDS at N = 197: 2 x 28 KiB images + 13 x 7 KiB dS^T tiles + lse/delta = 149 KiB (1 WG/CU).
+// ---------------------------------------------------------------------------
+template <int NT> struct BwdF {
+  static constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32, THREADS = NT * 64;
+  static constexpr int IMG = ROWS * 128, DST = ROWS * 32;
+  static constexpr int LDS = 2 * IMG + NT * DST + 2 * ROWS * 4;
+};
+
+template <int NT>
+__global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
+    const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H, int N, float scale, const bf16* __restrict__ o,
+    int64_t ld_o, const bf16* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
+    float* __restrict__ delta_out, bf16* __restrict__ dqkv, int64_t ld_dqkv, float* __restrict__ bias_part,
+    int causal) {
+  using F = BwdF<NT>;
+  constexpr int NT2 = F::NT2, ROWS = F::ROWS, NTHR = F::THREADS;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Qimg = smem;  // Q in phase 1, K in phase 2
+  char* Oimg = smem + F::IMG;  // dO
+  char* dST = smem + 2 * F::IMG;
+  float* lse2 = reinterpret_cast<float*>(dST + NT * F::DST);
+  float* delta = lse2 + ROWS;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l15 = lane & 15;
+  const bf16* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  const bf16* dob = dout + (int64_t)b * N * ld_do + h * 64;
+  const bf16* obase = o + (int64_t)b * N * ld_o + h * 64;
+
+  // ---- prologue: this wave's key tile (registers), Q / dO images, delta, lse
+  const int key = wave * 16 + l15;
+  const bool kvalid = key < N;
+  bf16x8 kf[2], vf[2];
+  {
+    const int kc = min(key, N - 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      kf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)kc * ld_qkv + D + kk * 32 + g * 8);
+      vf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)kc * ld_qkv + 2 * D + kk * 32 + g * 8);
+    }
+  }
+  {
+    constexpr int TOTAL = ROWS * 8, PER = (TOTAL + NTHR - 1) / NTHR;
+    bf16x8 qv[PER], dv8[PER], ov[PER];
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + u * NTHR;
+      const int row = min(idx >> 3, N - 1), c = idx & 7;
+      if (idx < TOTAL) {
+        qv[u] = *reinterpret_cast<const bf16x8*>(base + (int64_t)row * ld_qkv + c * 8);
+        dv8[u] = *reinterpret_cast<const bf16x8*>(dob + (int64_t)row * ld_do + c * 8);
+        ov[u] = *reinterpret_cast<const bf16x8*>(obase + (int64_t)row * ld_o + c * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PER; ++u) {
+      const int idx = tid + u * NTHR;
+      const int row = idx >> 3, c = idx & 7;
+      const bool in = idx < TOTAL, live = in && row < N;
+      float dl = 0.f;
+      if (live) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dl = fmaf((float)dv8[u][e], (float)ov[u][e], dl);
+      }
+      // the 8 chunks of a row sit in 8 consecutive lanes (NTHR % 8 == 0): reduce outside the branch
+      dl += __shfl_xor(dl, 1, 64);
+      dl += __shfl_xor(dl, 2, 64);
+      dl += __shfl_xor(dl, 4, 64);
+      if (in) {
+        bf16x8 qw = qv[u], dw = dv8[u];
+        if (!live) {
+#pragma unroll
+          for (int t = 0; t < 8; ++t) { qw[t] = (bf16)0.f; dw[t] = (bf16)0.f; }
+        }
+        *reinterpret_cast<bf16x8*>(Qimg + at_off(row, c)) = qw;
+        *reinterpret_cast<bf16x8*>(Oimg + at_off(row, c)) = dw;
+        if (c == 0) {
+          delta[row] = dl;
+          lse2[row] = live ? lse[(int64_t)bh * N + row] * LOG2E : INFINITY;
+          if (live) delta_out[(int64_t)bh * N + row] = dl;
+        }
+      }
+    }
+    // dS^T rows of the padded keys [NT*16, ROWS) are read by phase 2's last key pair: zero them
+    constexpr int PAD = (ROWS - NT * 16) * 32 / 16;  // 16-B chunks per column tile
+    if constexpr (PAD > 0) {
+      for (int i = tid; i < NT * PAD; i += NTHR) {
+        const int t = i / PAD, r = i - t * PAD;
+        *reinterpret_cast<f32x4*>(dST + t * F::DST + NT * 16 * 32 + r * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+  const AtOffsets off(lane);
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+
+  // ---- phase 1: wave = key tile
+  f32x4 dv[4], dk[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) { dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[dt] = dv[dt]; }
+  char* dsw = dST + key * 32 + g * 8;  // this lane's dS^T slot (queries 4g..4g+3 of a column tile)
+#pragma unroll 1
+  for (int qp = 0; qp < NT2; ++qp) {
+    f32x4 p[2], ds[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int qt = 2 * qp + u;
+      f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dpacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        sacc = mfma16(rowf(Qimg, qt * 16, off.row[kk]), kf[kk], sacc);
+        dpacc = mfma16(rowf(Oimg, qt * 16, off.row[kk]), vf[kk], dpacc);
+      }
+      const f32x4 l2 = *reinterpret_cast<const f32x4*>(lse2 + qt * 16 + 4 * g);
+      const f32x4 dl = *reinterpret_cast<const f32x4*>(delta + qt * 16 + 4 * g);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pv = kvalid ? fexp2(fmaf(sacc[r], c2, -l2[r])) : 0.f;
+        if (causal && key > qt * 16 + 4 * g + r) pv = 0.f;
+        p[u][r] = pv;
+        ds[u][r] = pv * (dpacc[r] - dl[r]);
+      }
+      if (qt < NT) {  // wave-uniform (the padded tile of an odd NT has no column tile)
+        const bf16x4 w = {(bf16)ds[u][0], (bf16)ds[u][1], (bf16)ds[u][2], (bf16)ds[u][3]};
+        *reinterpret_cast<bf16x4*>(dsw + qt * F::DST) = w;
+      }
+    }
+    const bf16x8 pf = pack8(p[0], p[1]), dsf = pack8(ds[0], ds[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dv[dt] = mfma16(trf(Oimg, qp * 32, off.tr[dt]), pf, dv[dt]);
+      dk[dt] = mfma16(trf(Qimg, qp * 32, off.tr[dt]), dsf, dk[dt]);
+    }
+  }
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) {
+    dk[dt] = kvalid ? dk[dt] * scale : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (!kvalid) dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (kvalid) {
+    bf16* row = dqkv + ((int64_t)b * N + key) * ld_dqkv + h * 64;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      bf16x4 kv = {(bf16)dk[dt][0], (bf16)dk[dt][1], (bf16)dk[dt][2], (bf16)dk[dt][3]};
+      bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
+      *reinterpret_cast<bf16x4*>(row + D + dt * 16 + 4 * g) = kv;
+      *reinterpret_cast<bf16x4*>(row + 2 * D + dt * 16 + 4 * g) = vv;
+    }
+  }
+  float cs[3] = {0.f, 0.f, 0.f};  // compressed column sums of dq, dk, dv (qkv-bias gradient)
+  if (bias_part) {
+    cs[1] = colsum16(dk, lane);
+    cs[2] = colsum16(dv, lane);
+  }
+  __syncthreads();  // every wave is done with Q, dO and has written its dS^T rows
+
+  // ---- phase 2: K tiles over the Q image (padded rows: zeros), wave = query tile
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    bf16x8 w = kf[kk];
+    if (!kvalid) {
+#pragma unroll
+      for (int t = 0; t < 8; ++t) w[t] = (bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(Qimg + at_off(key, kk * 4 + g)) = w;
+  }
+  __syncthreads();
+  {
+    const int q = wave * 16 + l15;
+    const char* dsr = dST + wave * F::DST + (4 * g + (l15 >> 2)) * 32 + (l15 & 3) * 8;
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kp = 0; kp < NT2; ++kp) {
+      const bf16x8 sf = cat4(lds_read_tr(dsr + kp * 32 * 32), lds_read_tr(dsr + kp * 32 * 32 + 16 * 32));
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma16(trf(Qimg, kp * 32, off.tr[dt]), sf, dq[dt]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = q < N ? dq[dt] * scale : f32x4{0.f, 0.f, 0.f, 0.f};
+    if (q < N) {
+      bf16* row = dqkv + ((int64_t)b * N + q) * ld_dqkv + h * 64;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        bf16x4 qv4 = {(bf16)dq[dt][0], (bf16)dq[dt][1], (bf16)dq[dt][2], (bf16)dq[dt][3]};
+        *reinterpret_cast<bf16x4*>(row + dt * 16 + 4 * g) = qv4;
+      }
+    }
+    if (bias_part) cs[0] = colsum16(dq, lane);
+  }
+  if (bias_part) {  // [3][NT][64] partials through LDS, then one 64-column row per output
+    float* red = reinterpret_cast<float*>(smem);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 3; ++t) red[(t * NT + wave) * 64 + colsum16_col(lane)] = cs[t];
+    __syncthreads();
+    for (int i = tid; i < 3 * 64; i += NTHR) {
+      const int t = i >> 6, d = i & 63;
+      float sum = 0.f;
+#pragma unroll
+      for (int w = 0; w < NT; ++w) sum += red[(t * NT + w) * 64 + d];
+      bias_part[(int64_t)b * 3 * D + t * D + h * 64 + d] = sum;
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -862,10 +1080,31 @@ static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N,
   VIT_CHECK_LAUNCH();
   return 0;
 }
+// VIT_ATTN_BWD_SPLIT=1 keeps the two-kernel backward for every N (A/B runs)
+static bool attn_bwd_split() {
+  static const int v = [] { const char* e = getenv("VIT_ATTN_BWD_SPLIT"); return e && *e == '1' ? 1 : 0; }();
+  return v != 0;
+}
+
 template <int NT>
 static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, int causal, const void* o,
                     int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, float* delta,
                     void* dqkv, int64_t ld_dqkv, float* bias_part, hipStream_t s) {
+  if constexpr (NT <= 14) {
+    if (!attn_bwd_split()) {
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)attn_bwd_fused<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  BwdF<NT>::LDS);
+        attr = true;
+      }
+      hipLaunchKernelGGL((attn_bwd_fused<NT>), dim3(B * H), dim3(BwdF<NT>::THREADS), BwdF<NT>::LDS, s,
+                         (const bf16*)qkv, ld_qkv, D, H, N, scale, (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse,
+                         delta, (bf16*)dqkv, ld_dqkv, bias_part, causal);
+      VIT_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   hipLaunchKernelGGL((attn_bwd_dq<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
                      (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, delta, (bf16*)dqkv, ld_dqkv, bias_part, causal);
   VIT_CHECK_LAUNCH();
