@@ -1,6 +1,10 @@
 """Per-dispatch HBM traffic of one kernel from rocprofv3 counter CSVs.
 
-    python tools/pmc_traffic.py <dir with *_counter_collection.csv> <kernel-name substring> [--out f.json]
+    python tools/pmc_traffic.py <dir with *_counter_collection.csv> <kernel-name substring>[,<substring>...] [--out f.json]
+
+With several comma-separated substrings (a kernel and its companion launches, e.g. the split-K
+weight gradient and its slab reduce) the per-dispatch averages of each are summed: traffic per
+call of the operation.
 
 FETCH_SIZE / WRITE_SIZE are rocprofv3's derived counters in KiB per dispatch.
 Correction applied (MI355X_MICROARCH.md, HBM section): on gfx950 FETCH_SIZE
@@ -29,12 +33,15 @@ def collect(d, sub):
 
 
 def main():
-    d, sub = sys.argv[1], sys.argv[2]
+    d, subs = sys.argv[1], sys.argv[2].split(",")
     out = sys.argv[sys.argv.index("--out") + 1] if "--out" in sys.argv else None
-    vals, names = collect(d, sub)
-    res = {"kernel_match": sub, "kernels": sorted(names), "dispatches": {k: len(v) for k, v in vals.items()}}
-    for k, v in vals.items():
-        res[k + "_KiB_avg"] = sum(v) / len(v)
+    res = {"kernel_match": subs, "kernels": [], "dispatches": {}}
+    for sub in subs:
+        vals, names = collect(d, sub)
+        res["kernels"] += sorted(names)
+        for k, v in vals.items():
+            res["dispatches"][sub + ":" + k] = len(v)
+            res[k + "_KiB_avg"] = res.get(k + "_KiB_avg", 0.0) + sum(v) / len(v)
     fetch = res.get("FETCH_SIZE_KiB_avg")
     write = res.get("WRITE_SIZE_KiB_avg")
     if fetch is not None:
