@@ -511,6 +511,24 @@ __device__ __forceinline__ bf16x8 asm_read128(uint32_t a) {
   asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
   return __builtin_bit_cast(bf16x8, v);
 }
+// the same read with a compile-time byte offset in the instruction's 16-bit offset field: the
+// fragments of one wave differ from each other only by such constants (below), so the loop
+// needs one address VGPR per k-substep instead of one v_add per fragment read
+template <int OFF> __device__ __forceinline__ bf16x8 asm_read128_off(uint32_t a) {
+  static_assert(OFF >= 0 && OFF < 65536, "ds_read offset field");
+  i32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+  return __builtin_bit_cast(bf16x8, v);
+}
+template <int N> struct Unroll {
+  template <class F> __device__ __forceinline__ static void run(F&& f) {
+    Unroll<N - 1>::run(f);
+    f(std::integral_constant<int, N - 1>{});
+  }
+};
+template <> struct Unroll<0> {
+  template <class F> __device__ __forceinline__ static void run(F&&) {}
+};
 __device__ __forceinline__ bf16x4 asm_read_tr(uint32_t a) {
   i32x2 v;
   asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
@@ -583,10 +601,41 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
 #pragma unroll
     for (int b = 0; b < C::AJ; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // staging sources: a k-independent per-lane byte offset of each 1-KiB piece (stage()'s
+  // addressing) plus a wave-uniform base advanced per k-step, so the loads take the SGPR-base
+  // form with no per-piece 64-bit address arithmetic (host side guarantees offsets < 2^32)
+  uint32_t poff[C::GP], qoff[C::GQ];
+  auto lane_offsets = [&](auto lay_tag, auto rows_tag, uint32_t* off, int G_OP, int64_t ld, int row0, int lim) {
+    constexpr int LAY = decltype(lay_tag)::value, ROWS = decltype(rows_tag)::value;
+    for (int u = 0; u < G_OP; ++u) {
+      const int t = wave * G_OP + u;
+      if constexpr (LAY == LAY_RC) {
+        constexpr int CPR = BK / 8, RPI = 64 / CPR;
+        const int row = t * RPI + lane / CPR;
+        const int c = (lane % CPR) ^ rc_sw<BK>(row);
+        off[u] = (uint32_t)((int64_t)min(row0 + row, lim - 1) * ld * 2 + c * 16);
+      } else {
+        constexpr int CPR = ROWS / 8, RPI = 64 / CPR;
+        const int r = t * RPI + lane / CPR;
+        const int c = cr_swz(lane % CPR, r);
+        off[u] = (uint32_t)((int64_t)r * ld * 2 + min(row0 + c * 8, lim - 8) * 2);
+      }
+    }
+  };
+  lane_offsets(std::integral_constant<int, PL>{}, std::integral_constant<int, BM>{}, poff, C::GP, ldp, i0, M);
+  lane_offsets(std::integral_constant<int, QL>{}, std::integral_constant<int, BN>{}, qoff, C::GQ, ldq, j0, N);
   auto issue = [&](int k) {
     char* buf = smem + (k % S) * C::STAGE;
-    stage<PL, BM, BK, C::GP>(buf, P, ldp, i0, rb + k * BK, M, wave, lane);
-    stage<QL, BN, BK, C::GQ>(buf + C::PIMG, Q, ldq, j0, rb + k * BK, N, wave, lane);
+    const int r = rb + k * BK;
+    const char* pb = reinterpret_cast<const char*>(P) + (PL == LAY_RC ? (int64_t)r * 2 : (int64_t)r * ldp * 2);
+    const char* qb = reinterpret_cast<const char*>(Q) + (QL == LAY_RC ? (int64_t)r * 2 : (int64_t)r * ldq * 2);
+#pragma unroll
+    for (int u = 0; u < C::GP; ++u)
+      __builtin_amdgcn_global_load_lds((const void*)(pb + poff[u]), LDS_PTR(buf + (wave * C::GP + u) * 1024), 16, 0, 0);
+#pragma unroll
+    for (int u = 0; u < C::GQ; ++u)
+      __builtin_amdgcn_global_load_lds((const void*)(qb + qoff[u]), LDS_PTR(buf + C::PIMG + (wave * C::GQ + u) * 1024), 16,
+                                       0, 0);
   };
   auto load_frags = [&](int k, int kk, bf16x8 (&pf)[C::AI], bf16x8 (&qf)[C::AJ]) {
     const char* cur = smem + (k % S) * C::STAGE;
@@ -602,6 +651,15 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
       for (int b = 0; b < C::AJ; ++b) acc[a][b] = mfma16(qf[b], pf[a], acc[a][b]);
   };
 
+  // lane part of the r-contiguous fragment addresses: rc_off(s*16 + l15, kk*4 + g) =
+  // s*16*BK*2 + rc_off(l15, kk*4 + g) for the wave's first fragment s, because the swizzle
+  // rc_sw(row) depends on row mod 16 only
+  uint32_t rc_lane[2][C::KS];
+#pragma unroll
+  for (int kk = 0; kk < C::KS; ++kk) {
+    rc_lane[0][kk] = (uint32_t)(wi * C::AI * 16 * BK * 2 + rc_off<BK>(lane & 15, kk * 4 + (lane >> 4)));
+    rc_lane[1][kk] = (uint32_t)(wj * C::AJ * 16 * BK * 2 + rc_off<BK>(lane & 15, kk * 4 + (lane >> 4)));
+  }
   if (nk > 0) {
 #pragma unroll
     for (int k = 0; k < S - 1; ++k)
@@ -617,10 +675,26 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
           // retired before the MFMAs, so they are also done before the next barrier (WAR)
           const uint32_t cur = lds_addr(smem + (kt % S) * C::STAGE);
           bf16x8 pf[C::AI], qf[C::AJ];
+          if constexpr (QL == LAY_RC) {  // fragment b = lane base + b * 16 rows (immediate)
+            const uint32_t qa = cur + C::PIMG + rc_lane[1][kk];
+            Unroll<C::AJ>::run([&](auto bI) {
+              constexpr int b = decltype(bI)::value;
+              qf[b] = asm_read128_off<b * 16 * BK * 2>(qa);
+            });
+          } else {
 #pragma unroll
-          for (int b = 0; b < C::AJ; ++b) qf[b] = frag_asm<QL, BN, BK>(cur + C::PIMG, wj * C::AJ + b, kk, lane);
+            for (int b = 0; b < C::AJ; ++b) qf[b] = frag_asm<QL, BN, BK>(cur + C::PIMG, wj * C::AJ + b, kk, lane);
+          }
+          if constexpr (PL == LAY_RC) {
+            const uint32_t pa = cur + rc_lane[0][kk];
+            Unroll<C::AI>::run([&](auto aI) {
+              constexpr int a = decltype(aI)::value;
+              pf[a] = asm_read128_off<a * 16 * BK * 2>(pa);
+            });
+          } else {
 #pragma unroll
-          for (int a = 0; a < C::AI; ++a) pf[a] = frag_asm<PL, BM, BK>(cur, wi * C::AI + a, kk, lane);
+            for (int a = 0; a < C::AI; ++a) pf[a] = frag_asm<PL, BM, BK>(cur, wi * C::AI + a, kk, lane);
+          }
           lgkm_wait0();
           mma(pf, qf);
         }
