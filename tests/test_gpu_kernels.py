@@ -378,6 +378,36 @@ def test_sdpa_fwd_bwd(N, dtype):
     _close(g[:, 2 * D:], dv, rel, "dv")
 
 
+# the fused bf16 backward walks several (b, h) items per workgroup once B*H >= 1024 (next item's
+# operands fetched during phase 2): 2 items at B*H = 1092, 4 with a ragged last workgroup at 1555
+@pytest.mark.parametrize("B,H,N,causal", [(91, 12, 197, False), (311, 5, 197, False), (311, 5, 224, True),
+                                          (256, 4, 130, False)])
+def test_sdpa_bwd_multi_item(B, H, N, causal):
+    D = H * 64
+    g = torch.Generator(device=DEV).manual_seed(36)
+    qkv = (torch.randn(B * N, 3 * D, device=DEV, generator=g) * 1.5).to(torch.bfloat16)
+    do = torch.randn(B * N, D, device=DEV, generator=g).to(torch.bfloat16)
+    q, k, v = qkv.float().reshape(B, N, 3, H, 64).permute(2, 0, 3, 1, 4)
+    q, k, v = [t.clone().requires_grad_(True) for t in (q, k, v)]
+    s = (q @ k.transpose(-2, -1)) * 0.125
+    if causal:
+        s = s + torch.full((N, N), float("-inf"), device=DEV).triu_(1)
+    lse = torch.logsumexp(s, -1).reshape(-1)
+    o_ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B * N, D)
+    o_ref.backward(do.float())
+    dbias = torch.empty(3 * D, device=DEV)
+    dqkv = ops.sdpa_bwd(qkv, o_ref.detach().to(torch.bfloat16), do, lse.detach(), B, H, N, dbias=dbias,
+                        causal=causal)
+    ref = torch.cat([t.grad.transpose(1, 2).reshape(B * N, D) for t in (q, k, v)], 1)
+    _close(dqkv.float(), ref, 3e-2, "dqkv")
+    _close(dbias, ref.sum(0), 3e-2, "qkv bias grad")
+    # every head's rows, not just the global norm: the worst head's relative error
+    err = (dqkv.float() - ref).reshape(B, N, 3, H, 64).permute(0, 3, 2, 1, 4).reshape(B * H, -1)
+    scl = ref.reshape(B, N, 3, H, 64).permute(0, 3, 2, 1, 4).reshape(B * H, -1)
+    worst = (err.norm(dim=1) / scl.norm(dim=1).clamp_min(1e-6)).max().item()
+    assert worst < 3e-2, f"worst (b, h) item rel err {worst}"
+
+
 @pytest.mark.parametrize("N", [77, 16, 197, 224])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_sdpa_causal_fwd_bwd(N, dtype):

@@ -96,13 +96,34 @@ __device__ __forceinline__ bf16x8 trf(const char* img, int row0, int off) {
 }
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// Diagnostic phase stamps (tools/attn_stamps.py): a separate template instance, launched only
+// while vit_debug_attn_stamps() has set a buffer.  Thread 0 of a workgroup records s_memtime at
+// phase boundaries and s_memrealtime at start / end into stamps[blockIdx.x * 8 + i].
+static unsigned long long* g_attn_stamps = nullptr;
+#define AT_STAMP(i)                                                   \
+  if constexpr (STAMP) { if (threadIdx.x == 0) st[i] = __builtin_amdgcn_s_memtime(); }
+#define AT_STAMP_BEGIN()                                                                          \
+  unsigned long long st[8] = {0, 0, 0, 0, 0, 0, 0, 0};                                            \
+  if constexpr (STAMP) { if (threadIdx.x == 0) st[5] = __builtin_amdgcn_s_memrealtime(); }        \
+  AT_STAMP(0)
+#define AT_STAMP_FLUSH()                                                                         \
+  if constexpr (STAMP) if (threadIdx.x == 0) {                                                   \
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                                             \
+    st[6] = __builtin_amdgcn_s_memtime();                                                        \
+    st[7] = __builtin_amdgcn_s_memrealtime();                                                    \
+    unsigned long long* d = stamps + (int64_t)blockIdx.x * 8;                                    \
+    for (int i_ = 0; i_ < 8; ++i_) d[i_] = st[i_];                                               \
+  }
+
 // ---------------------------------------------------------------------------
 // bf16 forward
 // ---------------------------------------------------------------------------
-template <int NT>  // key/query tiles of 16: NT = ceil(N/16)
+template <int NT, bool STAMP = false>  // key/query tiles of 16: NT = ceil(N/16)
 __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(const bf16* __restrict__ qkv, int64_t ld_qkv, int D,
                                                      int H, int N, float scale, bf16* __restrict__ o,
-                                                     int64_t ld_o, float* __restrict__ lse, int causal) {
+                                                     int64_t ld_o, float* __restrict__ lse, int causal,
+                                                     unsigned long long* __restrict__ stamps) {
+  AT_STAMP_BEGIN()
   constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32;
   __shared__ __attribute__((aligned(16))) char smem[2 * ROWS * 128];
   char* Kimg = smem;
@@ -118,6 +139,7 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
   }
   const AtOffsets off(lane);
   __syncthreads();
+  AT_STAMP(1)
   const float c2 = scale * LOG2E;
   for (int qt = wave; qt < NT; qt += AT_WAVES) {
     const int q = qt * 16 + (lane & 15);
@@ -146,19 +168,23 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
         for (int r = 0; r < 4; ++r)
           if (kt * 16 + 4 * g + r > q) s[kt][r] = -INFINITY;
     }
-    float m = -INFINITY;
+    // row max / sum as 4 independent chains (one per accumulator slot r): a single chain over
+    // the 4*NT scores is a 52-deep dependent VALU sequence at N = 197
+    float mr[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) m = fmaxf(m, s[kt][r]);
+      for (int r = 0; r < 4; ++r) mr[r] = fmaxf(mr[r], s[kt][r]);
+    float m = fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3]));
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
     const float mc = m * c2;
-    float l = 0.f;
+    float lr[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int kt = 0; kt < NT; ++kt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) { float p = fexp2(fmaf(s[kt][r], c2, -mc)); s[kt][r] = p; l += p; }
+      for (int r = 0; r < 4; ++r) { float p = fexp2(fmaf(s[kt][r], c2, -mc)); s[kt][r] = p; lr[r] += p; }
+    float l = (lr[0] + lr[1]) + (lr[2] + lr[3]);
     l += __shfl_xor(l, 16, 64);
     l += __shfl_xor(l, 32, 64);
     f32x4 oacc[4];
@@ -184,6 +210,8 @@ __global__ __launch_bounds__(AT_THREADS, NT <= 14 ? 4 : 2) void attn_fwd_mfma(co
       if (g == 0) lse[(int64_t)bh * N + q] = (mc + __log2f(l)) * LN2;
     }
   }
+  AT_STAMP(2)
+  AT_STAMP_FLUSH()
 }
 
 
@@ -690,12 +718,13 @@ template <int NT> struct BwdF {
   static constexpr int LDS = 2 * IMG + NT * DST + 2 * ROWS * 4;
 };
 
-template <int NT>
+template <int NT, bool CAUSAL = false, bool STAMP = false>
 __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
     const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H, int N, float scale, const bf16* __restrict__ o,
     int64_t ld_o, const bf16* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
     float* __restrict__ delta_out, bf16* __restrict__ dqkv, int64_t ld_dqkv, float* __restrict__ bias_part,
-    int causal) {
+    unsigned long long* __restrict__ stamps) {
+  AT_STAMP_BEGIN()
   using F = BwdF<NT>;
   constexpr int NT2 = F::NT2, ROWS = F::ROWS, NTHR = F::THREADS;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -758,8 +787,9 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
         *reinterpret_cast<bf16x8*>(Qimg + at_off(row, c)) = qw;
         *reinterpret_cast<bf16x8*>(Oimg + at_off(row, c)) = dw;
         if (c == 0) {
-          delta[row] = dl;
-          lse2[row] = live ? lse[(int64_t)bh * N + row] * LOG2E : INFINITY;
+          // negated row constants: the initial S / dP accumulators of phase 1
+          delta[row] = -dl;
+          lse2[row] = live ? -lse[(int64_t)bh * N + row] / scale : -INFINITY;
           if (live) delta_out[(int64_t)bh * N + row] = dl;
         }
       }
@@ -775,6 +805,7 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
   }
   const AtOffsets off(lane);
   __syncthreads();
+  AT_STAMP(1)
   const float c2 = scale * LOG2E;
 
   // ---- phase 1: wave = key tile
@@ -788,20 +819,22 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int qt = 2 * qp + u;
-      f32x4 sacc = {0.f, 0.f, 0.f, 0.f}, dpacc = {0.f, 0.f, 0.f, 0.f};
+      // row constants as the initial accumulators: S' = QK^T - lse/scale (-inf on padded keys),
+      // dP' = dO V^T - delta, so p = exp2(c2 S') and dS = p dP' (two VALU ops per element)
+      const f32x4 nl = *reinterpret_cast<const f32x4*>(lse2 + qt * 16 + 4 * g);
+      f32x4 sacc = kvalid ? nl : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+      f32x4 dpacc = *reinterpret_cast<const f32x4*>(delta + qt * 16 + 4 * g);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk) {
         sacc = mfma16(rowf(Qimg, qt * 16, off.row[kk]), kf[kk], sacc);
         dpacc = mfma16(rowf(Oimg, qt * 16, off.row[kk]), vf[kk], dpacc);
       }
-      const f32x4 l2 = *reinterpret_cast<const f32x4*>(lse2 + qt * 16 + 4 * g);
-      const f32x4 dl = *reinterpret_cast<const f32x4*>(delta + qt * 16 + 4 * g);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float pv = kvalid ? fexp2(fmaf(sacc[r], c2, -l2[r])) : 0.f;
-        if (causal && key > qt * 16 + 4 * g + r) pv = 0.f;
+        float pv = fexp2(sacc[r] * c2);
+        if constexpr (CAUSAL) { if (key > qt * 16 + 4 * g + r) pv = 0.f; }
         p[u][r] = pv;
-        ds[u][r] = pv * (dpacc[r] - dl[r]);
+        ds[u][r] = pv * dpacc[r];
       }
       if (qt < NT) {  // wave-uniform (the padded tile of an odd NT has no column tile)
         const bf16x4 w = {(bf16)ds[u][0], (bf16)ds[u][1], (bf16)ds[u][2], (bf16)ds[u][3]};
@@ -836,6 +869,7 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
     cs[2] = colsum16(dv, lane);
   }
   __syncthreads();  // every wave is done with Q, dO and has written its dS^T rows
+  AT_STAMP(2)
 
   // ---- phase 2: K tiles over the Q image (padded rows: zeros), wave = query tile
 #pragma unroll
@@ -848,6 +882,7 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
     *reinterpret_cast<bf16x8*>(Qimg + at_off(key, kk * 4 + g)) = w;
   }
   __syncthreads();
+  AT_STAMP(3)
   {
     const int q = wave * 16 + l15;
     const char* dsr = dST + wave * F::DST + (4 * g + (l15 >> 2)) * 32 + (l15 & 3) * 8;
@@ -886,6 +921,8 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
       bias_part[(int64_t)b * 3 * D + t * D + h * 64 + d] = sum;
     }
   }
+  AT_STAMP(4)
+  AT_STAMP_FLUSH()
 }
 
 // ---------------------------------------------------------------------------
@@ -1075,8 +1112,12 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const T* __restrict__ o
 template <int NT>
 static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, int causal, void* o,
                     int64_t ld_o, float* lse, hipStream_t s) {
-  hipLaunchKernelGGL((attn_fwd_mfma<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N, scale,
-                     (bf16*)o, ld_o, lse, causal);
+  if (g_attn_stamps)
+    hipLaunchKernelGGL((attn_fwd_mfma<NT, true>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H,
+                       N, scale, (bf16*)o, ld_o, lse, causal, g_attn_stamps);
+  else
+    hipLaunchKernelGGL((attn_fwd_mfma<NT>), dim3(B * H), dim3(AT_THREADS), 0, s, (const bf16*)qkv, ld_qkv, D, H, N,
+                       scale, (bf16*)o, ld_o, lse, causal, nullptr);
   VIT_CHECK_LAUNCH();
   return 0;
 }
@@ -1096,11 +1137,23 @@ static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N,
       if (!attr) {
         (void)hipFuncSetAttribute((const void*)attn_bwd_fused<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   BwdF<NT>::LDS);
+        (void)hipFuncSetAttribute((const void*)attn_bwd_fused<NT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  BwdF<NT>::LDS);
+        (void)hipFuncSetAttribute((const void*)attn_bwd_fused<NT, false, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, BwdF<NT>::LDS);
         attr = true;
       }
-      hipLaunchKernelGGL((attn_bwd_fused<NT>), dim3(B * H), dim3(BwdF<NT>::THREADS), BwdF<NT>::LDS, s,
-                         (const bf16*)qkv, ld_qkv, D, H, N, scale, (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse,
-                         delta, (bf16*)dqkv, ld_dqkv, bias_part, causal);
+#define BWD_FUSED(C, S, ST)                                                                                    \
+  hipLaunchKernelGGL((attn_bwd_fused<NT, C, S>), dim3(B * H), dim3(BwdF<NT>::THREADS), BwdF<NT>::LDS, s,         \
+                     (const bf16*)qkv, ld_qkv, D, H, N, scale, (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, \
+                     delta, (bf16*)dqkv, ld_dqkv, bias_part, ST)
+      if (causal)
+        BWD_FUSED(true, false, nullptr);
+      else if (g_attn_stamps)
+        BWD_FUSED(false, true, g_attn_stamps);
+      else
+        BWD_FUSED(false, false, nullptr);
+#undef BWD_FUSED
       VIT_CHECK_LAUNCH();
       return 0;
     }
@@ -1117,6 +1170,13 @@ static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N,
 #define NT_CASES(X) X(1) X(2) X(3) X(4) X(5) X(6) X(7) X(8) X(9) X(10) X(11) X(12) X(13) X(14) X(15) X(16) X(17) X(18)
 
 extern "C" {
+
+// diagnostic only (tools/attn_stamps.py): phase stamps of the bf16 forward / fused backward
+// kernels go to buf ([B*H][8] u64) until called again with null; not part of include/vit_hip.h
+int vit_debug_attn_stamps(void* buf) {
+  g_attn_stamps = (unsigned long long*)buf;
+  return 0;
+}
 
 // F.scaled_dot_product_attention(q, k, v) (no dropout) for head_dim 64; causal = 1
 // masks key > query (OpenAI CLIP text tower attn_mask, additive -inf above the diagonal).
