@@ -378,11 +378,11 @@ def test_sdpa_fwd_bwd(N, dtype):
     _close(g[:, 2 * D:], dv, rel, "dv")
 
 
-# the fused bf16 backward walks several (b, h) items per workgroup once B*H >= 1024 (next item's
-# operands fetched during phase 2): 2 items at B*H = 1092, 4 with a ragged last workgroup at 1555
+# the fused bf16 backward at step-sized grids (B*H = 1024 .. 1555 workgroups, causal and padded
+# key tiles), every (b, h) item checked on its own against torch fp32 autograd
 @pytest.mark.parametrize("B,H,N,causal", [(91, 12, 197, False), (311, 5, 197, False), (311, 5, 224, True),
                                           (256, 4, 130, False)])
-def test_sdpa_bwd_multi_item(B, H, N, causal):
+def test_sdpa_bwd_large_grid(B, H, N, causal):
     D = H * 64
     g = torch.Generator(device=DEV).manual_seed(36)
     qkv = (torch.randn(B * N, 3 * D, device=DEV, generator=g) * 1.5).to(torch.bfloat16)
