@@ -322,6 +322,29 @@ def test_layer_norm_fwd_bwd(D, xdt):
     _close(db, br.grad, 1e-5, "dbeta")
 
 
+@pytest.mark.parametrize("D", [768, 1024])
+def test_add_layer_norm_fwd(D):
+    """xs = x + r (f32 + bf16), y = LayerNorm(xs) in bf16, mean/rstd; in place (xs is x) and add-only."""
+    M = 333
+    x = _rnd(M, D, seed=30, scale=2.0)
+    r = _rnd(M, D, seed=31).to(torch.bfloat16)
+    w = 1 + _rnd(D, seed=32, scale=0.2)
+    b = _rnd(D, seed=33, scale=0.1)
+    s = x + r.float()
+    yr = torch.nn.functional.layer_norm(s, (D,), w, b, 1e-6)
+    xs = torch.empty(M, D, device=DEV)
+    y = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+    mean, rstd = torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.add_layer_norm_fwd(x.to(DEV), r.to(DEV), xs, w.to(DEV), b.to(DEV), 1e-6, out=y, mean=mean, rstd=rstd)
+    _close(xs, s, 0, "sum")  # one f32 add: exact
+    _close(y, yr, 8e-3, "ln")
+    _close(mean, s.mean(1), 1e-5, "mean")
+    _close(rstd, 1 / (s.var(1, unbiased=False) + 1e-6).sqrt(), 1e-5, "rstd")
+    xi = x.to(DEV)
+    ops.add_layer_norm_fwd(xi, r.to(DEV), xi)  # add only, in place
+    _close(xi, s, 0, "in-place add")
+
+
 def test_layer_norm_bwd_compact_rows():
     B, S, D = 3, 5, 768
     x = _rnd(B * S, D, seed=30)

@@ -1139,14 +1139,14 @@ static int env_variant(const char* name) {
 // per-shape choice among the kept configurations (sweep on MI355X, bs=256 ViT-B/16 shapes)
 static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool pers_ok, bool act_bwd) {
   static const int o_fwd = env_variant("VIT_GEMM_FWD"), o_dgrad = env_variant("VIT_GEMM_DGRAD"),
-                   o_wgrad = env_variant("VIT_GEMM_WGRAD");
+                   o_wgrad = env_variant("VIT_GEMM_WGRAD"), o_fwd_small = env_variant("VIT_GEMM_FWD_SMALL");
   const bool wgrad = split > 1 || (pl == LAY_CR && ql == LAY_CR), fwd = pl == LAY_RC && ql == LAY_RC;
   const int o = wgrad ? o_wgrad : fwd ? o_fwd : o_dgrad;
   int v;
   if (g_variant >= 0) v = g_variant % 100;
   else if (o >= 0) v = o;
   else if (wgrad) v = 8;                                                   // wgrad: ping-pong 256x256
-  else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : 2;                     // forward
+  else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : (o_fwd_small >= 0 ? o_fwd_small : 2);  // forward
   else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;                // dgrad (GELU' epilogue: V1, 2 WG/CU)
   (void)M;
   if ((v == 2 || v == 5 || v == 10) && R % 64) v = 1;                       // BK = 64 configurations need 64-row chunks

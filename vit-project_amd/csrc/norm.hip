@@ -82,6 +82,55 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, i
   }
 }
 
+// Residual add + LayerNorm forward (bf16 step): s = x + r with x the f32 residual
+// stream and r a Linear's bf16 output (bias included) -- the Linear's f32 output under autocast
+// rounded to bf16, then added in f32 as timm's `x + attn(...)` / `x + mlp(...)` does -- written to
+// xs (f32, may alias x), and y = LN(s) (bf16, optional: y == null writes only the sum).  One wave per
+// row; the Linear's epilogue then stores 2 bytes per element instead of reading and writing the
+// f32 stream (4 + 4), and that traffic moves into this streaming kernel.
+template <int NV>
+__global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict__ x, int64_t ldx,
+                                                         const bf16* __restrict__ r, int64_t ldr,
+                                                         float* __restrict__ xs, int64_t ldxs, bf16* __restrict__ y,
+                                                         int64_t ldy, const float* __restrict__ w,
+                                                         const float* __restrict__ b, float* __restrict__ mean,
+                                                         float* __restrict__ rstd, int rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (int64_t)row * ldx;
+  const bf16* rr = r + (int64_t)row * ldr;
+  float* sr = xs + (int64_t)row * ldxs;
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = col4(lane, k);
+    v[k] = ld4<float>(xr + c) + ld4<bf16>(rr + c);
+    s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
+  }
+#pragma unroll
+  for (int k = 0; k < NV; ++k) st4<float>(sr + col4(lane, k), v[k]);
+  if (y == nullptr) return;
+  const float mu = wave_sum(s) / D;
+  float q = 0.f;
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { float d = v[k][t] - mu; q += d * d; }
+  const float rs = rsqrtf(wave_sum(q) / D + eps);
+  bf16* yr = y + (int64_t)row * ldy;
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    const int c = col4(lane, k);
+    f32x4 g = *reinterpret_cast<const f32x4*>(w + c), bb = *reinterpret_cast<const f32x4*>(b + c), o;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) o[t] = (v[k][t] - mu) * rs * g[t] + bb[t];
+    st4<bf16>(yr + c, o);
+  }
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+}
+
 __device__ __forceinline__ bool copy_row(int row, int compact_np, int64_t& orow) {
   orow = row;
   if (compact_np > 0) {
@@ -268,6 +317,33 @@ int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x,
   else if (dtype_x == VIT_F32) launch_fwd<float, bf16>(nv, grid, s, x, ldx, y, ldy, w, b, mean, rstd, rows, D, eps);
   else if (dtype_y == VIT_BF16) launch_fwd<bf16, bf16>(nv, grid, s, x, ldx, y, ldy, w, b, mean, rstd, rows, D, eps);
   else launch_fwd<bf16, float>(nv, grid, s, x, ldx, y, ldy, w, b, mean, rstd, rows, D, eps);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+// xs = x + r (f32 + bf16 -> f32; xs may alias x) and, when y is non-null, y = LayerNorm(xs) (bf16)
+// with its mean / rstd: the residual add of a Linear's bf16 output fused into the LayerNorm that
+// follows it.  D must be a multiple of 256 (ViT-B 768, ViT-L 1024) and every stride of 4 elements.
+int vit_add_layer_norm_fwd(int rows, int D, const float* x, int64_t ldx, const void* r, int64_t ldr, float* xs,
+                           int64_t ldxs, void* y, int64_t ldy, const float* w, const float* b, float* mean,
+                           float* rstd, float eps, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (rows <= 0) return 0;
+  if (D % 256 || D > 2048 || (ldx | ldr | ldxs | ldy) % 4) return (int)hipErrorInvalidValue;
+  if (y && (!w || !b || !mean || !rstd)) return (int)hipErrorInvalidValue;
+  dim3 grid((rows + LN_WAVES - 1) / LN_WAVES);
+#define A(NV) hipLaunchKernelGGL((add_ln_fwd_kernel<NV>), grid, dim3(64 * LN_WAVES), 0, s, x, ldx, (const bf16*)r, ldr, xs, \
+                                 ldxs, (bf16*)y, ldy, w, b, mean, rstd, rows, D, eps)
+  switch (D / 256) {
+    case 1: A(1); break;
+    case 2: A(2); break;
+    case 3: A(3); break;
+    case 4: A(4); break;
+    case 6: A(6); break;
+    case 8: A(8); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef A
   VIT_CHECK_LAUNCH();
   return 0;
 }

@@ -81,6 +81,11 @@ _FWD_STAGGER = [int(os.environ.get("VIT_FWD_STAGGER", "0"))]
 _HOLD = {}
 
 
+# VIT_FUSED_RESID=0: the proj / fc2 GEMMs add into the f32 residual stream in their epilogue
+# (EPI_RESID) instead of the following LayerNorm doing it (A/B runs)
+_FUSED_RESID = [os.environ.get("VIT_FUSED_RESID", "1") != "0"]
+
+
 def set_wgrad_overlap(enable: bool):
     """Run weight/bias gradients on a side stream (default) or inline on the caller's stream."""
     _OVERLAP[0] = bool(enable)
@@ -273,8 +278,44 @@ class _BlockFn(torch.autograd.Function):
         causal = bool(cfg.get("causal", False))
         attn_fp8 = bool(cfg.get("attn_fp8", False))  # forward-only blocks (frozen prefix, no-grad passes)
 
+        # fused residual adds (bf16 ViT, VisionTransformer._tokens): proj / fc2 store their bf16 output
+        # (bias included) and the add into the f32 stream runs inside the next LayerNorm -- norm2 here,
+        # the next block's norm1 for fc2 (this block's output xo is then written by that kernel), or
+        # an add-only launch after the last block.  rs["pending"]: the previous block's (xm, fc2 out).
+        rs = cfg.get("resid")
+        pend = rs.get("pending") if rs is not None else None
+        pb = yb = None
+        if rs is not None:
+            pb, yb = torch.empty(M, D, dtype=T, device=dev), torch.empty(M, D, dtype=T, device=dev)
+
+        def ln1(sl):
+            if pend is not None:
+                return lambda: ops.add_layer_norm_fwd(pend[0][sl], pend[1][sl], x2[sl], n1w.detach(), n1b.detach(), eps,
+                                                      out=h1[sl], mean=m1[sl], rstd=r1[sl])
+            return lambda: ops.layer_norm_fwd(x2[sl], n1w.detach(), n1b.detach(), eps, T, out=h1[sl], mean=m1[sl],
+                                              rstd=r1[sl])
+
+        def chain_fused(b0, b1):
+            sl = slice(b0 * N, b1 * N)
+            steps = [
+                ln1(sl),
+                lambda: ops.linear_fwd(h1[sl], Wqkv, qkvb.detach(), out=qkv[sl]),
+                lambda: ops.sdpa_fwd(qkv[sl], b1 - b0, H, N, o=o[sl], lse=lse[b0 * H * N:b1 * H * N], causal=causal,
+                                     fp8=attn_fp8),
+                lambda: ops.linear_fwd(o[sl], Wproj, projb.detach(), out=pb[sl]),
+                lambda: ops.add_layer_norm_fwd(x2[sl], pb[sl], xm[sl], n2w.detach(), n2b.detach(), eps, out=h2[sl],
+                                               mean=m2[sl], rstd=r2[sl]),
+                lambda: ops.linear_fwd(h2[sl], W1, fc1b.detach(), epi=act_epi, out=dact[sl], act_out=act[sl]),
+                lambda: ops.linear_fwd(act[sl], W2, fc2b.detach(), out=yb[sl]),
+            ]
+            if cfg.get("resid_last"):
+                steps.append(lambda: ops.add_layer_norm_fwd(xm[sl], yb[sl], xo[sl]))
+            return steps
+
         def chain(b0, b1):
             """The block over images [b0, b1) (rows b0*N .. b1*N of every tensor) as its 7 launches."""
+            if rs is not None:
+                return chain_fused(b0, b1)
             r0, r1_ = b0 * N, b1 * N
             sl = slice(r0, r1_)
             return [
@@ -306,7 +347,8 @@ class _BlockFn(torch.autograd.Function):
             k = max(0, min(len(mine), _FWD_STAGGER[0]))
             run(mine[:k])
             side.run(lambda: run(other))
-            side.guard(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act, xo)
+            side.guard(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act, xo,
+                       *(t for t in (pb, yb, *(pend or ())) if t is not None))
             run(mine[k:])
             # each half only feeds the same half of the next block: a stack of blocks joins
             # once after its last block (cfg "defer_join", ViT._tokens) instead of per block
@@ -314,6 +356,8 @@ class _BlockFn(torch.autograd.Function):
                 side.join()
         else:
             run(chain(0, B))
+        if rs is not None:
+            rs["pending"] = None if cfg.get("resid_last") else (xm, yb)
         ctx.save_for_backward(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act)
         ctx.params = (n1w, n1b, qkvw, qkvb, projw, projb, n2w, n2b, fc1w, fc1b, fc2w, fc2b)
         ctx.wops = (Wqkv, Wproj, W1, W2)
@@ -644,8 +688,13 @@ class VisionTransformer(nn.Module):
         hook = getattr(self, "_grad_hook", None) if cfg["defer_bwd_join"] else None
         # fp8 attention (set_attention_fp8): forward passes that build no graph (eval / RSA)
         cfg["attn_fp8"] = self._attn_fp8 and not torch.is_grad_enabled()
+        D = self.embed_dim
+        if _FUSED_RESID[0] and self.compute_dtype != torch.float32 and D % 256 == 0:
+            cfg["resid"] = {"pending": None}  # residual adds inside the LayerNorms (_BlockFn.forward)
         for i, blk in enumerate(self.blocks):
             bcfg = cfg if i != 0 else dict(cfg, compact_np=pe.num_patches)
+            if "resid" in cfg and i == n - 1:
+                bcfg = dict(bcfg, resid_last=True)
             if hook is not None:
                 bcfg = dict(bcfg, grad_hook=hook, flat_span=blk._flat_span)
             x = _BlockFn.apply(x, *blk.block_params(), bcfg)

@@ -189,6 +189,18 @@ def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, nee
     return out, mean, rstd
 
 
+def add_layer_norm_fwd(x2d, r2d, xs, w=None, b=None, eps=1e-6, out=None, mean=None, rstd=None):
+    """xs = x2d + r2d (f32 + bf16 -> f32; xs may be x2d) and, with ``out`` given, out = LayerNorm(xs)
+    (bf16) with its row mean / rstd: a Linear's residual add fused into the LayerNorm after it."""
+    assert x2d.dtype == torch.float32 and xs.dtype == torch.float32 and r2d.dtype == torch.bfloat16
+    rows, D = xs.shape
+    if out is not None:
+        assert out.dtype == torch.bfloat16 and mean is not None and rstd is not None
+    call("vit_add_layer_norm_fwd", rows, D, ptr(x2d), x2d.stride(0), ptr(r2d), r2d.stride(0), ptr(xs), xs.stride(0),
+         ptr(out), out.stride(0) if out is not None else 0, ptr(w), ptr(b), ptr(mean), ptr(rstd), float(eps), _s(xs))
+    return xs
+
+
 _LN_MULTI = [os.environ.get("VIT_LN_MULTI", "1") != "0"]
 
 
