@@ -67,6 +67,8 @@ _OVERLAP = [True]
 # forward half-batch chains: join the two streams after every block ("block") or once after
 # the block stack ("end", default)
 _FWD_JOIN = [os.environ.get("VIT_FWD_JOIN", "end")]
+# VIT_FWD_SPLIT=0: the forward as one full-batch chain on the caller's stream (A/B runs)
+_FWD_SPLIT = [os.environ.get("VIT_FWD_SPLIT", "1") != "0"]
 # block backward: join the side stream (weight/bias gradients) at the end of every block
 # ("block") or once, in the patch embedding's backward ("end": flat-gradient runs only)
 _BWD_JOIN = [os.environ.get("VIT_BWD_JOIN", "end")]
@@ -336,7 +338,7 @@ class _BlockFn(torch.autograd.Function):
                 f()
 
         side = _Side(dev)
-        if side.on and B >= 2 and T != torch.float32:
+        if side.on and B >= 2 and T != torch.float32 and _FWD_SPLIT[0]:
             # two half-batch chains on two streams: one chain's GEMM epilogues (HBM-bound)
             # overlap the other's MFMA main loops.  The side chain is released (side.run waits for
             # everything the caller's stream has queued) after the caller's first _FWD_STAGGER
