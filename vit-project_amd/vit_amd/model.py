@@ -93,13 +93,38 @@ def set_wgrad_overlap(enable: bool):
     _OVERLAP[0] = bool(enable)
 
 
+# VIT_SIDE_CUS=k (A/B only): the side stream restricted to k of the 256 CUs by a HIP CU mask
+# (hipExtStreamCreateWithCUMask; k spread evenly over the mask bits), instead of dynamic sharing
+_SIDE_CUS = [int(os.environ.get("VIT_SIDE_CUS", "0"))]
+
+
+def _side_stream(dev):
+    k = _SIDE_CUS[0]
+    if k <= 0:
+        return torch.cuda.Stream(device=dev)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    bits = [(i * k) // ncu != ((i + 1) * k) // ncu for i in range(ncu)]  # k of ncu, evenly spread
+    words = (ctypes.c_uint32 * ((ncu + 31) // 32))()
+    for i, on in enumerate(bits):
+        if on:
+            words[i // 32] |= 1 << (i % 32)
+    handle = ctypes.c_void_p()
+    with torch.cuda.device(dev):
+        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), words)
+    if rc != 0:
+        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
+    return torch.cuda.ExternalStream(handle.value, device=dev)
+
+
 class _Side:
     def __init__(self, dev):
         self.main = torch.cuda.current_stream(dev)
         self.on = _OVERLAP[0] and dev.type == "cuda"
         if self.on:
             if dev not in _SIDE:
-                _SIDE[dev] = torch.cuda.Stream(device=dev)
+                _SIDE[dev] = _side_stream(dev)
             self.side = _SIDE[dev]
 
     def run(self, fn):
