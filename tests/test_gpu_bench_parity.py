@@ -2,11 +2,11 @@
 
 bench.py's step (VIT:132-147): ViT-B/16, bs=256, compute_dtype bf16, flat gradients,
 deferred weight-gradient join, the forward as two half-batch chains on two streams
-(images [0, 136) on the caller's stream, [136, 256) on the side stream at the default
-VIT_FWD_HALF_DELTA = B/32: M = 26 792 / 23 640 token rows, ragged GEMM tiles).
+(images [0, 140) on the caller's stream, [140, 256) on the side stream at the default
+VIT_FWD_HALF_DELTA = 3B/64, model.fwd_split: M = 27 580 / 22 852 token rows, ragged GEMM tiles).
 
   (a) per-image logits and CLS features for images on both sides of the chain split
-      {0, 1, 135, 136, 254, 255} against the CPU fp32 oracle run on those images alone
+      {0, 1, hb-1, hb, 254, 255} against the CPU fp32 oracle run on those images alone
       (the forward is per-image independent): max error <= 3e-2 of the row's scale and
       cosine >= 0.999;
   (b) every parameter gradient of the bs=256 bf16 step against the HIP fp32 path on the same
@@ -26,7 +26,9 @@ from oracle import vit_ref as R  # noqa: E402
 
 DEV = "cuda"
 B = 256
-IDX = [0, 1, 135, 136, 254, 255]
+from vit_amd import model as _VM  # noqa: E402
+_HB = _VM.fwd_split(B)
+IDX = [0, 1, _HB - 1, _HB, 254, 255]
 
 
 @pytest.fixture(scope="module", autouse=True)
