@@ -1137,15 +1137,18 @@ static int env_variant(const char* name) {
 }
 
 // per-shape choice among the kept configurations (sweep on MI355X, bs=256 ViT-B/16 shapes)
-static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool pers_ok, bool act_bwd) {
+static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool pers_ok, bool act_bwd,
+                        bool act_fwd = false) {
   static const int o_fwd = env_variant("VIT_GEMM_FWD"), o_dgrad = env_variant("VIT_GEMM_DGRAD"),
-                   o_wgrad = env_variant("VIT_GEMM_WGRAD"), o_fwd_small = env_variant("VIT_GEMM_FWD_SMALL");
+                   o_wgrad = env_variant("VIT_GEMM_WGRAD"), o_fwd_small = env_variant("VIT_GEMM_FWD_SMALL"),
+                   o_fwd_gelu = env_variant("VIT_GEMM_FWD_GELU");
   const bool wgrad = split > 1 || (pl == LAY_CR && ql == LAY_CR), fwd = pl == LAY_RC && ql == LAY_RC;
   const int o = wgrad ? o_wgrad : fwd ? o_fwd : o_dgrad;
   int v;
   if (g_variant >= 0) v = g_variant % 100;
   else if (o >= 0) v = o;
   else if (wgrad) v = 8;                                                   // wgrad: ping-pong 256x256
+  else if (fwd && act_fwd && o_fwd_gelu >= 0) v = o_fwd_gelu;               // forward with the GELU pair
   else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : (o_fwd_small >= 0 ? o_fwd_small : 2);  // forward
   else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;                // dgrad (GELU' epilogue: V1, 2 WG/CU)
   (void)M;
@@ -1235,7 +1238,8 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
                        int split, const Epi& e, hipStream_t s) {
   constexpr bool pers_ok = PL == LAY_RC && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU ||
                                             EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
-  const int v = pick_variant(PL, QL, M, N, R, split, pers_ok, EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
+  const int v = pick_variant(PL, QL, M, N, R, split, pers_ok, EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD,
+                             EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU);
   if constexpr (pers_ok) {
     // the persistent kernel's buffer-descriptor stores need full column tiles and 32-bit offsets
     if (v == 10 && N % pers::C::BN == 0 && (int64_t)M * e.ldc * (int64_t)sizeof(TO) < ((int64_t)1 << 31))
