@@ -926,6 +926,136 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
 }
 
 // ---------------------------------------------------------------------------
+// f32 forward on v_mfma_f32_16x16x4_f32 (CLIP-HBA at the reference's fp32 precision, NEWP:274;
+// config C3): one workgroup (8 waves) per (b, h), K and V of the head in LDS as f32 (<= 2 x 72 KiB,
+// N <= 288), wave = query tile of 16.  Products are exact f32 (the MFMA's f32 form), accumulation f32.
+//   S^T = K Q^T: A = K (row = key), B = Q^T; the 4 k-slots of lane group g take head dims 16g + ks, so a
+//     lane reads 16 consecutive floats of its key row (4 x ds_read_b128) and holds Q[query][16g..16g+15]
+//     in registers.  Output: lane (l15, g) holds S[query l15][key 4g + r] -- the bf16 kernel's layout.
+//   O^T = V^T P^T: B = P^T straight from the softmax registers (k-slot g at step (kt, r) is key
+//     kt*16 + 4g + r, the key the lane already holds); A row m of d-tile dt is head dim 4m + dt, so one
+//     ds_read_b128 of V[key][4*l15 .. 4*l15+3] feeds the 4 d-tiles, and a lane ends with
+//     O[query l15][16g .. 16g+15].
+// K image: 16-B chunk c of row r at chunk position c ^ kswz(r) -- conflict-free for the four
+// ds_read_b128 of a key tile (each 16-lane group covers 16 rows and two chunk columns); V image plain
+// row-major (a group reads one row and its 4th-next, disjoint banks).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int kswz(int r) {
+  const int x = r & 15;
+  return x ^ ((((x >> 2) ^ (x >> 3)) & 1) << 2);
+}
+
+template <int NT>
+__global__ __launch_bounds__(512) void attn_fwd_f32mfma(const float* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                        int N, float scale, float* __restrict__ o, int64_t ld_o,
+                                                        float* __restrict__ lse, int causal) {
+  constexpr int ROWS = NT * 16, KG = 4;  // key tiles per K-register group
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Kimg = reinterpret_cast<float*>(smem);
+  float* Vimg = Kimg + ROWS * 64;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l15 = lane & 15;
+  const float* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  // K, V -> LDS (rows >= N zero)
+  for (int i = tid; i < ROWS * 16; i += 512) {
+    const int r = i >> 4, c = i & 15;
+    f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = kv;
+    if (r < N) {
+      kv = *reinterpret_cast<const f32x4*>(base + (int64_t)r * ld_qkv + D + c * 4);
+      vv = *reinterpret_cast<const f32x4*>(base + (int64_t)r * ld_qkv + 2 * D + c * 4);
+    }
+    *reinterpret_cast<f32x4*>(Kimg + r * 64 + ((c ^ kswz(r)) << 2)) = kv;
+    *reinterpret_cast<f32x4*>(Vimg + r * 64 + c * 4) = vv;
+  }
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  for (int qt = wave; qt < NT; qt += 8) {
+    const int q = qt * 16 + l15;
+    float qf[16];
+    {
+      const float* qr = base + (int64_t)min(q, N - 1) * ld_qkv + 16 * g;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(qr + 4 * j);
+        qf[4 * j] = v[0]; qf[4 * j + 1] = v[1]; qf[4 * j + 2] = v[2]; qf[4 * j + 3] = v[3];
+      }
+    }
+    f32x4 s[NT];
+#pragma unroll
+    for (int k0 = 0; k0 < NT; k0 += KG) {
+      float kf[KG][16];
+#pragma unroll
+      for (int u = 0; u < KG; ++u) {
+        if (k0 + u < NT) {
+          const int r = (k0 + u) * 16 + l15;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 v = *reinterpret_cast<const f32x4*>(Kimg + r * 64 + (((4 * g + j) ^ kswz(r)) << 2));
+            kf[u][4 * j] = v[0]; kf[u][4 * j + 1] = v[1]; kf[u][4 * j + 2] = v[2]; kf[u][4 * j + 3] = v[3];
+          }
+          s[k0 + u] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks)
+#pragma unroll
+        for (int u = 0; u < KG; ++u)
+          if (k0 + u < NT) s[k0 + u] = __builtin_amdgcn_mfma_f32_16x16x4f32(kf[u][ks], qf[ks], s[k0 + u], 0, 0, 0);
+    }
+    // keys >= N exist only in the last tile
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if ((NT - 1) * 16 + 4 * g + r >= N) s[NT - 1][r] = -INFINITY;
+    if (causal) {
+#pragma unroll
+      for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kt * 16 + 4 * g + r > q) s[kt][r] = -INFINITY;
+    }
+    float mr[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mr[r] = fmaxf(mr[r], s[kt][r]);
+    float m = fmaxf(fmaxf(mr[0], mr[1]), fmaxf(mr[2], mr[3]));
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float mc = m * c2;
+    float lr[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { const float p = fexp2(fmaf(s[kt][r], c2, -mc)); s[kt][r] = p; lr[r] += p; }
+    float l = (lr[0] + lr[1]) + (lr[2] + lr[3]);
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 oacc[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) oacc[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < NT; ++kt) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(Vimg + (kt * 16 + 4 * g + r) * 64 + 4 * l15);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) oacc[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(v[dt], s[kt][r], oacc[dt], 0, 0, 0);
+      }
+      if (kt % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // bound V-read hoisting (VGPRs)
+    }
+    if (q < N) {
+      const float inv = 1.0f / l;
+      float* orow = o + ((int64_t)b * N + q) * ld_o + h * 64 + 16 * g;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        *reinterpret_cast<f32x4*>(orow + 4 * rr) =
+            f32x4{oacc[0][rr] * inv, oacc[1][rr] * inv, oacc[2][rr] * inv, oacc[3][rr] * inv};
+      if (g == 0 && lse) lse[(int64_t)bh * N + q] = (mc + __log2f(l)) * LN2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // generic (f32 compute, f32 or bf16 storage) path: 4 lanes per query / key,
 // each owning 16 of the 64 head dims; keys / queries streamed through LDS.
 // ---------------------------------------------------------------------------
@@ -1121,6 +1251,25 @@ static int fwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N,
   VIT_CHECK_LAUNCH();
   return 0;
 }
+// VIT_ATTN_F32_GENERIC=1: the scalar-FMA f32 forward instead of the f32 MFMA kernel (A/B runs)
+static bool attn_f32_generic() {
+  static const int v = [] { const char* e = getenv("VIT_ATTN_F32_GENERIC"); return e && *e == '1' ? 1 : 0; }();
+  return v != 0;
+}
+template <int NT>
+static int fwd_f32mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, int causal, void* o,
+                       int64_t ld_o, float* lse, hipStream_t s) {
+  constexpr int lds = 2 * NT * 16 * 64 * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_fwd_f32mfma<NT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((attn_fwd_f32mfma<NT>), dim3(B * H), dim3(512), lds, s, (const float*)qkv, ld_qkv, D, H, N, scale,
+                     (float*)o, ld_o, lse, causal);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
 // VIT_ATTN_BWD_SPLIT=1 keeps the two-kernel backward for every N (A/B runs)
 static bool attn_bwd_split() {
   static const int v = [] { const char* e = getenv("VIT_ATTN_BWD_SPLIT"); return e && *e == '1' ? 1 : 0; }();
@@ -1191,6 +1340,14 @@ int vit_sdpa_fwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
     int nt = (N + 15) / 16;
     switch (nt) {
 #define CASE(n) case n: return fwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, causal, o, ld_o, lse, s);
+      NT_CASES(CASE)
+#undef CASE
+    }
+  }
+  if (dtype == VIT_F32 && (ld_qkv % 4 == 0) && (ld_o % 4 == 0) && !attn_f32_generic()) {
+    int nt = (N + 15) / 16;
+    switch (nt) {
+#define CASE(n) case n: return fwd_f32mfma<n>(qkv, ld_qkv, D, B, H, N, scale, causal, o, ld_o, lse, s);
       NT_CASES(CASE)
 #undef CASE
     }
