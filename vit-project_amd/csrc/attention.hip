@@ -1056,6 +1056,191 @@ __global__ __launch_bounds__(512) void attn_fwd_f32mfma(const float* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// f32 backward on v_mfma_f32_16x16x4_f32 (N <= 288, head_dim 64), the same operand algebra as the f32
+// forward: two kernels, each with two head images in LDS (kswz chunk swizzle, read both by rows -- 4
+// ds_read_b128 of 16 consecutive floats -- and by columns -- one ds_read_b128 of chunk l15 of row
+// 4g + r, the A operand of the 4 d-tiles whose row m is head dim 4m + dt).
+//   dq : wave = query tile, K and V images; S^T and dP^T with the lane's query in registers, so a lane
+//        holds keys 4g + r of query l15; dQ^T += K^T dS^T, B = dS^T from registers.  Writes delta.
+//   dkv: wave = key tile, Q and dO images; S and dP with the wave's key tile in registers (a lane
+//        holds queries 4g + r of key l15); dV^T += dO^T P, dK^T += Q^T dS, B from registers.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void f32_img_load(float* img, const float* src, int64_t ld, int N, int rows, int tid,
+                                             int nthr) {
+  for (int i = tid; i < rows * 16; i += nthr) {
+    const int r = i >> 4, c = i & 15;
+    f32x4 v = {0.f, 0.f, 0.f, 0.f};
+    if (r < N) v = *reinterpret_cast<const f32x4*>(src + (int64_t)r * ld + c * 4);
+    *reinterpret_cast<f32x4*>(img + r * 64 + ((c ^ kswz(r)) << 2)) = v;
+  }
+}
+// row r of a swizzled image: the 16 floats [16g, 16g + 16) (4 chunks)
+__device__ __forceinline__ void f32_row16(const float* img, int r, int g, float (&x)[16]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(img + r * 64 + (((4 * g + j) ^ kswz(r)) << 2));
+    x[4 * j] = v[0]; x[4 * j + 1] = v[1]; x[4 * j + 2] = v[2]; x[4 * j + 3] = v[3];
+  }
+}
+__device__ __forceinline__ f32x4 f32_chunk(const float* img, int r, int c) {
+  return *reinterpret_cast<const f32x4*>(img + r * 64 + ((c ^ kswz(r)) << 2));
+}
+__device__ __forceinline__ void f32_glob16(const float* p, float (&x)[16]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p + 4 * j);
+    x[4 * j] = v[0]; x[4 * j + 1] = v[1]; x[4 * j + 2] = v[2]; x[4 * j + 3] = v[3];
+  }
+}
+__device__ __forceinline__ f32x4 mfma4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int NT>
+__global__ __launch_bounds__(512) void attn_bwd_dq_f32mfma(const float* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                           int N, float scale, const float* __restrict__ o, int64_t ld_o,
+                                                           const float* __restrict__ dout, int64_t ld_do,
+                                                           const float* __restrict__ lse, float* __restrict__ delta_out,
+                                                           float* __restrict__ dqkv, int64_t ld_dqkv, int causal) {
+  constexpr int ROWS = NT * 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Kimg = reinterpret_cast<float*>(smem);
+  float* Vimg = Kimg + ROWS * 64;
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l15 = lane & 15;
+  const float* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  f32_img_load(Kimg, base + D, ld_qkv, N, ROWS, tid, 512);
+  f32_img_load(Vimg, base + 2 * D, ld_qkv, N, ROWS, tid, 512);
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  for (int qt = wave; qt < NT; qt += 8) {
+    const int q = qt * 16 + l15, qc = min(q, N - 1);
+    float qf[16], df[16], of[16];
+    f32_glob16(base + (int64_t)qc * ld_qkv + 16 * g, qf);
+    f32_glob16(dout + ((int64_t)b * N + qc) * ld_do + h * 64 + 16 * g, df);
+    f32_glob16(o + ((int64_t)b * N + qc) * ld_o + h * 64 + 16 * g, of);
+    float dl = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dl = fmaf(df[j], of[j], dl);
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    if (q < N && g == 0) delta_out[(int64_t)bh * N + q] = dl;
+    const float l2 = q < N ? lse[(int64_t)bh * N + q] * LOG2E : INFINITY;
+    f32x4 dq[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int kt = 0; kt < NT; ++kt) {
+      float kf[16], vf[16];
+      f32_row16(Kimg, kt * 16 + l15, g, kf);
+      f32_row16(Vimg, kt * 16 + l15, g, vf);
+      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = st;
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        st = mfma4(kf[ks], qf[ks], st);   // S^T[key 4g + r][query l15]
+        dpt = mfma4(vf[ks], df[ks], dpt);
+      }
+      f32x4 ds;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = kt * 16 + 4 * g + r;
+        float p = key < N ? fexp2(fmaf(st[r], c2, -l2)) : 0.f;
+        if (causal && key > q) p = 0.f;
+        ds[r] = p * (dpt[r] - dl);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f32x4 a = f32_chunk(Kimg, kt * 16 + 4 * g + r, l15);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) dq[dt] = mfma4(a[dt], ds[r], dq[dt]);
+      }
+    }
+    if (q < N) {
+      float* row = dqkv + ((int64_t)b * N + q) * ld_dqkv + h * 64 + 16 * g;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        *reinterpret_cast<f32x4*>(row + 4 * rr) =
+            f32x4{dq[0][rr] * scale, dq[1][rr] * scale, dq[2][rr] * scale, dq[3][rr] * scale};
+    }
+  }
+}
+
+template <int NT>
+__global__ __launch_bounds__(512) void attn_bwd_dkv_f32mfma(const float* __restrict__ qkv, int64_t ld_qkv, int D, int H,
+                                                            int N, float scale, const float* __restrict__ dout,
+                                                            int64_t ld_do, const float* __restrict__ lse,
+                                                            const float* __restrict__ delta, float* __restrict__ dqkv,
+                                                            int64_t ld_dqkv, int causal) {
+  constexpr int ROWS = NT * 16;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* Qimg = reinterpret_cast<float*>(smem);
+  float* Oimg = Qimg + ROWS * 64;  // dO
+  float* l2s = Oimg + ROWS * 64;   // lse * log2(e) per query (+inf past N)
+  float* dls = l2s + ROWS;         // delta per query
+  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l15 = lane & 15;
+  const float* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
+  f32_img_load(Qimg, base, ld_qkv, N, ROWS, tid, 512);
+  f32_img_load(Oimg, dout + (int64_t)b * N * ld_do + h * 64, ld_do, N, ROWS, tid, 512);
+  for (int i = tid; i < ROWS; i += 512) {
+    l2s[i] = i < N ? lse[(int64_t)bh * N + i] * LOG2E : INFINITY;
+    dls[i] = i < N ? delta[(int64_t)bh * N + i] : 0.f;
+  }
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  for (int kt = wave; kt < NT; kt += 8) {
+    const int key = kt * 16 + l15, kc = min(key, N - 1);
+    const bool kvalid = key < N;
+    float kf[16], vf[16];
+    f32_glob16(base + (int64_t)kc * ld_qkv + D + 16 * g, kf);
+    f32_glob16(base + (int64_t)kc * ld_qkv + 2 * D + 16 * g, vf);
+    f32x4 dk[4], dv[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) { dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dv[dt] = dk[dt]; }
+#pragma unroll 1
+    for (int qt = 0; qt < NT; ++qt) {
+      float qf[16], df[16];
+      f32_row16(Qimg, qt * 16 + l15, g, qf);
+      f32_row16(Oimg, qt * 16 + l15, g, df);
+      f32x4 sc = {0.f, 0.f, 0.f, 0.f}, dpc = sc;
+#pragma unroll
+      for (int ks = 0; ks < 16; ++ks) {
+        sc = mfma4(qf[ks], kf[ks], sc);   // S[query 4g + r][key l15]
+        dpc = mfma4(df[ks], vf[ks], dpc);
+      }
+      const f32x4 l2 = *reinterpret_cast<const f32x4*>(l2s + qt * 16 + 4 * g);
+      const f32x4 dl = *reinterpret_cast<const f32x4*>(dls + qt * 16 + 4 * g);
+      f32x4 p, ds;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float pv = kvalid ? fexp2(fmaf(sc[r], c2, -l2[r])) : 0.f;
+        if (causal && key > qt * 16 + 4 * g + r) pv = 0.f;
+        p[r] = pv;
+        ds[r] = pv * (dpc[r] - dl[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const f32x4 ao = f32_chunk(Oimg, qt * 16 + 4 * g + r, l15), aq = f32_chunk(Qimg, qt * 16 + 4 * g + r, l15);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          dv[dt] = mfma4(ao[dt], p[r], dv[dt]);
+          dk[dt] = mfma4(aq[dt], ds[r], dk[dt]);
+        }
+      }
+    }
+    if (kvalid) {
+      float* row = dqkv + ((int64_t)b * N + key) * ld_dqkv + h * 64 + 16 * g;
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        *reinterpret_cast<f32x4*>(row + D + 4 * rr) =
+            f32x4{dk[0][rr] * scale, dk[1][rr] * scale, dk[2][rr] * scale, dk[3][rr] * scale};
+        *reinterpret_cast<f32x4*>(row + 2 * D + 4 * rr) = f32x4{dv[0][rr], dv[1][rr], dv[2][rr], dv[3][rr]};
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // generic (f32 compute, f32 or bf16 storage) path: 4 lanes per query / key,
 // each owning 16 of the 64 head dims; keys / queries streamed through LDS.
 // ---------------------------------------------------------------------------
@@ -1270,6 +1455,25 @@ static int fwd_f32mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int
   VIT_CHECK_LAUNCH();
   return 0;
 }
+template <int NT>
+static int bwd_f32mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, int causal,
+                       const void* o, int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, float* delta,
+                       void* dqkv, int64_t ld_dqkv, hipStream_t s) {
+  constexpr int img = NT * 16 * 64 * 4, lds_dq = 2 * img, lds_dkv = 2 * img + 2 * NT * 16 * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dq_f32mfma<NT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_dq);
+    (void)hipFuncSetAttribute((const void*)attn_bwd_dkv_f32mfma<NT>, hipFuncAttributeMaxDynamicSharedMemorySize, lds_dkv);
+    attr = true;
+  }
+  hipLaunchKernelGGL((attn_bwd_dq_f32mfma<NT>), dim3(B * H), dim3(512), lds_dq, s, (const float*)qkv, ld_qkv, D, H, N,
+                     scale, (const float*)o, ld_o, (const float*)dout, ld_do, lse, delta, (float*)dqkv, ld_dqkv, causal);
+  VIT_CHECK_LAUNCH();
+  hipLaunchKernelGGL((attn_bwd_dkv_f32mfma<NT>), dim3(B * H), dim3(512), lds_dkv, s, (const float*)qkv, ld_qkv, D, H,
+                     N, scale, (const float*)dout, ld_do, lse, (const float*)delta, (float*)dqkv, ld_dqkv, causal);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
 // VIT_ATTN_BWD_SPLIT=1 keeps the two-kernel backward for every N (A/B runs)
 static bool attn_bwd_split() {
   static const int v = [] { const char* e = getenv("VIT_ATTN_BWD_SPLIT"); return e && *e == '1' ? 1 : 0; }();
@@ -1416,6 +1620,18 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
     if (rc || !dbias) return rc;
     launch_colreduce(partial, B, 3 * D, dbias, 0, s, partial + (int64_t)B * 3 * D);
     VIT_CHECK_LAUNCH();
+    return 0;
+  }
+  if (dtype == VIT_F32 && (ld_qkv % 4 == 0) && (ld_do % 4 == 0) && (ld_dqkv % 4 == 0) && (ld_o % 4 == 0) &&
+      !attn_f32_generic()) {
+    int nt = (N + 15) / 16, rc = (int)hipErrorInvalidValue;
+    switch (nt) {
+#define CASE(n) case n: rc = bwd_f32mfma<n>(qkv, ld_qkv, D, B, H, N, scale, causal, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, s); break;
+      NT_CASES(CASE)
+#undef CASE
+    }
+    if (rc) return rc;
+    if (dbias) return vit_colsum(dtype, B * N, 3 * D, dqkv, ld_dqkv, dbias, partial, partial_floats, 0, stream);
     return 0;
   }
   dim3 grid((N + 63) / 64, B * H);
