@@ -44,7 +44,7 @@ import torch.nn as nn
 from . import _lib as L
 from . import ops
 from .dora import DoRALayer
-from .model import _BlockFn, _Shadowed, _gout, _wt
+from .model import _FUSED_RESID, _BlockFn, _Shadowed, _gout, _wt
 
 SOT, EOT = 49406, 49407
 
@@ -331,8 +331,14 @@ class CLIP(nn.Module):
         heads = W // 64
         blocks = list(v.transformer.resblocks)
         first = _first_trainable(blocks)
+        # bf16: the residual adds run inside the next LayerNorm (as the ViT blocks, model._tokens);
+        # f32 keeps the GEMM's residual epilogue (the reference's precision, NEWP:274)
+        rs = {"pending": None} if (_FUSED_RESID[0] and T != torch.float32 and W % 256 == 0) else None
         for i, blk in enumerate(blocks):
-            x = _BlockFn.apply(x, *blk.block_params(), self._cfg(heads, False, frozen=i < first))
+            cfg = self._cfg(heads, False, frozen=i < first)
+            if rs is not None:
+                cfg = dict(cfg, resid=rs, resid_last=i == len(blocks) - 1)
+            x = _BlockFn.apply(x, *blk.block_params(), cfg)
         idx = self._cls_rows(B, npatch + 1, x.device)
         return _PoolHeadFn.apply(x, idx, v.ln_post.weight, v.ln_post.bias, v.proj, 1e-5)
 
