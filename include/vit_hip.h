@@ -96,14 +96,14 @@ int vit_pos_grad(int B, int S, int D, const float* dx, float* dpos, float* dcls,
 int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x, int64_t ldx, void* y,
                        int64_t ldy, const float* w, const float* b, float* mean, float* rstd, float eps,
                        void* stream);
-/* xs = x + r (f32 residual stream + a Linear's bf16 output, bias included; xs may alias x) and, when y
- * is non-null, y = LayerNorm(xs) in bf16 with mean/rstd: timm Block's `x = x + attn(norm1(x))` /
+/* xs = x + r (f32 residual stream + a Linear's output (dtype_r bf16 or f32), bias included; xs may alias
+ * x) and, when y is non-null, y = LayerNorm(xs) (dtype_y) with mean/rstd: timm Block's `x = x + attn(norm1(x))` /
  * `x = x + mlp(norm2(x))` residual adds (VIT Block.forward via timm) fused into the LayerNorm that
  * follows them (norm2 of the same block, norm1 of the next); y == null: the add alone (last block).
  * D % 256 == 0, strides % 4 == 0. */
-int vit_add_layer_norm_fwd(int rows, int D, const float* x, int64_t ldx, const void* r, int64_t ldr, float* xs,
-                           int64_t ldxs, void* y, int64_t ldy, const float* w, const float* b, float* mean,
-                           float* rstd, float eps, void* stream);
+int vit_add_layer_norm_fwd(int dtype_r, int dtype_y, int rows, int D, const float* x, int64_t ldx, const void* r,
+                           int64_t ldr, float* xs, int64_t ldxs, void* y, int64_t ldy, const float* w, const float* b,
+                           float* mean, float* rstd, float eps, void* stream);
 /* LayerNorm backward with fused residual-gradient add, optional GEMM-dtype copy
  * of dx (optionally dropping CLS rows), dgamma/dbeta, and dsum = column sums of dx
  * (bias gradient of the Linear whose output fed the residual: proj / fc2). */

@@ -343,6 +343,13 @@ def test_add_layer_norm_fwd(D):
     xi = x.to(DEV)
     ops.add_layer_norm_fwd(xi, r.to(DEV), xi)  # add only, in place
     _close(xi, s, 0, "in-place add")
+    # f32 branch output and f32 LayerNorm output (the fp32 compute path)
+    rf = r.float() + _rnd(M, D, seed=34, scale=1e-3)
+    sf = x + rf
+    yf = torch.empty(M, D, device=DEV)
+    ops.add_layer_norm_fwd(x.to(DEV), rf.to(DEV), xs, w.to(DEV), b.to(DEV), 1e-6, out=yf, mean=mean, rstd=rstd)
+    _close(xs, sf, 0, "f32 sum")
+    _close(yf, torch.nn.functional.layer_norm(sf, (D,), w, b, 1e-6), 1e-5, "f32 ln")
 
 
 def test_layer_norm_bwd_compact_rows():

@@ -88,10 +88,10 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const TX* __restrict__ x, i
 // xs (f32, may alias x), and y = LN(s) (bf16, optional: y == null writes only the sum).  One wave per
 // row; the Linear's epilogue then stores 2 bytes per element instead of reading and writing the
 // f32 stream (4 + 4), and that traffic moves into this streaming kernel.
-template <int NV>
+template <int NV, typename TR, typename TY>
 __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict__ x, int64_t ldx,
-                                                         const bf16* __restrict__ r, int64_t ldr,
-                                                         float* __restrict__ xs, int64_t ldxs, bf16* __restrict__ y,
+                                                         const TR* __restrict__ r, int64_t ldr,
+                                                         float* __restrict__ xs, int64_t ldxs, TY* __restrict__ y,
                                                          int64_t ldy, const float* __restrict__ w,
                                                          const float* __restrict__ b, float* __restrict__ mean,
                                                          float* __restrict__ rstd, int rows, int D, float eps) {
@@ -99,14 +99,14 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict
   const int row = blockIdx.x * LN_WAVES + (threadIdx.x >> 6);
   if (row >= rows) return;
   const float* xr = x + (int64_t)row * ldx;
-  const bf16* rr = r + (int64_t)row * ldr;
+  const TR* rr = r + (int64_t)row * ldr;
   float* sr = xs + (int64_t)row * ldxs;
   f32x4 v[NV];
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = col4(lane, k);
-    v[k] = ld4<float>(xr + c) + ld4<bf16>(rr + c);
+    v[k] = ld4<float>(xr + c) + ld4<TR>(rr + c);
     s += (v[k][0] + v[k][1]) + (v[k][2] + v[k][3]);
   }
 #pragma unroll
@@ -119,14 +119,14 @@ __global__ __launch_bounds__(256) void add_ln_fwd_kernel(const float* __restrict
 #pragma unroll
     for (int t = 0; t < 4; ++t) { float d = v[k][t] - mu; q += d * d; }
   const float rs = rsqrtf(wave_sum(q) / D + eps);
-  bf16* yr = y + (int64_t)row * ldy;
+  TY* yr = y + (int64_t)row * ldy;
 #pragma unroll
   for (int k = 0; k < NV; ++k) {
     const int c = col4(lane, k);
     f32x4 g = *reinterpret_cast<const f32x4*>(w + c), bb = *reinterpret_cast<const f32x4*>(b + c), o;
 #pragma unroll
     for (int t = 0; t < 4; ++t) o[t] = (v[k][t] - mu) * rs * g[t] + bb[t];
-    st4<bf16>(yr + c, o);
+    st4<TY>(yr + c, o);
   }
   if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
 }
@@ -321,28 +321,37 @@ int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x,
   return 0;
 }
 
-// xs = x + r (f32 + bf16 -> f32; xs may alias x) and, when y is non-null, y = LayerNorm(xs) (bf16)
+// xs = x + r (f32 + bf16 / f32 -> f32; xs may alias x) and, when y is non-null, y = LayerNorm(xs) (bf16 / f32)
 // with its mean / rstd: the residual add of a Linear's bf16 output fused into the LayerNorm that
 // follows it.  D must be a multiple of 256 (ViT-B 768, ViT-L 1024) and every stride of 4 elements.
-int vit_add_layer_norm_fwd(int rows, int D, const float* x, int64_t ldx, const void* r, int64_t ldr, float* xs,
-                           int64_t ldxs, void* y, int64_t ldy, const float* w, const float* b, float* mean,
-                           float* rstd, float eps, void* stream) {
+int vit_add_layer_norm_fwd(int dtype_r, int dtype_y, int rows, int D, const float* x, int64_t ldx, const void* r,
+                           int64_t ldr, float* xs, int64_t ldxs, void* y, int64_t ldy, const float* w, const float* b,
+                           float* mean, float* rstd, float eps, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   if (rows <= 0) return 0;
   if (D % 256 || D > 2048 || (ldx | ldr | ldxs | ldy) % 4) return (int)hipErrorInvalidValue;
   if (y && (!w || !b || !mean || !rstd)) return (int)hipErrorInvalidValue;
   dim3 grid((rows + LN_WAVES - 1) / LN_WAVES);
-#define A(NV) hipLaunchKernelGGL((add_ln_fwd_kernel<NV>), grid, dim3(64 * LN_WAVES), 0, s, x, ldx, (const bf16*)r, ldr, xs, \
-                                 ldxs, (bf16*)y, ldy, w, b, mean, rstd, rows, D, eps)
+  if ((dtype_r != VIT_BF16 && dtype_r != VIT_F32) || (dtype_y != VIT_BF16 && dtype_y != VIT_F32))
+    return (int)hipErrorInvalidValue;
+#define A(NV, TR, TY)                                                                                          \
+  hipLaunchKernelGGL((add_ln_fwd_kernel<NV, TR, TY>), grid, dim3(64 * LN_WAVES), 0, s, x, ldx, (const TR*)r, ldr, xs, \
+                     ldxs, (TY*)y, ldy, w, b, mean, rstd, rows, D, eps)
+#define AD(NV)                                                         \
+  if (dtype_r == VIT_BF16 && dtype_y == VIT_BF16) A(NV, bf16, bf16);   \
+  else if (dtype_r == VIT_BF16) A(NV, bf16, float);                    \
+  else if (dtype_y == VIT_BF16) A(NV, float, bf16);                    \
+  else A(NV, float, float);
   switch (D / 256) {
-    case 1: A(1); break;
-    case 2: A(2); break;
-    case 3: A(3); break;
-    case 4: A(4); break;
-    case 6: A(6); break;
-    case 8: A(8); break;
+    case 1: AD(1) break;
+    case 2: AD(2) break;
+    case 3: AD(3) break;
+    case 4: AD(4) break;
+    case 6: AD(6) break;
+    case 8: AD(8) break;
     default: return (int)hipErrorInvalidValue;
   }
+#undef AD
 #undef A
   VIT_CHECK_LAUNCH();
   return 0;

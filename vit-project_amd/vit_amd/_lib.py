@@ -36,7 +36,7 @@ SIGNATURES = {
     "vit_colsum": [i32, i32, i32, vp, i64, vp, vp, i64, i32, vp],
     "vit_patch_embed_fwd": [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
     "vit_layer_norm_fwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, f32, vp],
-    "vit_add_layer_norm_fwd": [i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, f32, vp],
+    "vit_add_layer_norm_fwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, f32, vp],
     "vit_layer_norm_bwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, i32,
                            i32, vp, vp, vp, vp, i64, i32, vp],
     "vit_layer_norm_bwd_partial_floats": [i32, i32],

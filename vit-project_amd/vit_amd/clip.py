@@ -44,7 +44,7 @@ import torch.nn as nn
 from . import _lib as L
 from . import ops
 from .dora import DoRALayer
-from .model import _FUSED_RESID, _BlockFn, _Shadowed, _gout, _wt
+from .model import _FUSED_RESID, _FUSED_RESID_F32, _BlockFn, _Shadowed, _gout, _wt
 
 SOT, EOT = 49406, 49407
 
@@ -331,9 +331,10 @@ class CLIP(nn.Module):
         heads = W // 64
         blocks = list(v.transformer.resblocks)
         first = _first_trainable(blocks)
-        # bf16: the residual adds run inside the next LayerNorm (as the ViT blocks, model._tokens);
-        # f32 keeps the GEMM's residual epilogue (the reference's precision, NEWP:274)
-        rs = {"pending": None} if (_FUSED_RESID[0] and T != torch.float32 and W % 256 == 0) else None
+        # the residual adds run inside the next LayerNorm (as the ViT blocks, model._tokens); in f32 the
+        # same f32 add as the GEMM's residual epilogue, so the reference-precision result is unchanged
+        rs = ({"pending": None} if (_FUSED_RESID[0] and (T != torch.float32 or _FUSED_RESID_F32[0]) and W % 256 == 0)
+              else None)
         for i, blk in enumerate(blocks):
             cfg = self._cfg(heads, False, frozen=i < first)
             if rs is not None:

@@ -86,6 +86,9 @@ _HOLD = {}
 # VIT_FUSED_RESID=0: the proj / fc2 GEMMs add into the f32 residual stream in their epilogue
 # (EPI_RESID) instead of the following LayerNorm doing it (A/B runs)
 _FUSED_RESID = [os.environ.get("VIT_FUSED_RESID", "1") != "0"]
+# ... and in fp32 compute with VIT_FUSED_RESID_F32=1 (bit-identical: the same f32 add, in the LayerNorm
+# instead of the epilogue; C3 fp32 measured 607 vs 609 img/s, so the f32 GEMM epilogue keeps it by default)
+_FUSED_RESID_F32 = [os.environ.get("VIT_FUSED_RESID_F32", "0") == "1"]
 
 
 def set_wgrad_overlap(enable: bool):
@@ -723,7 +726,7 @@ class VisionTransformer(nn.Module):
         # fp8 attention (set_attention_fp8): forward passes that build no graph (eval / RSA)
         cfg["attn_fp8"] = self._attn_fp8 and not torch.is_grad_enabled()
         D = self.embed_dim
-        if _FUSED_RESID[0] and self.compute_dtype != torch.float32 and D % 256 == 0:
+        if _FUSED_RESID[0] and (self.compute_dtype != torch.float32 or _FUSED_RESID_F32[0]) and D % 256 == 0:
             cfg["resid"] = {"pending": None}  # residual adds inside the LayerNorms (_BlockFn.forward)
         for i, blk in enumerate(self.blocks):
             bcfg = cfg if i != 0 else dict(cfg, compact_np=pe.num_patches)

@@ -190,13 +190,15 @@ def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, nee
 
 
 def add_layer_norm_fwd(x2d, r2d, xs, w=None, b=None, eps=1e-6, out=None, mean=None, rstd=None):
-    """xs = x2d + r2d (f32 + bf16 -> f32; xs may be x2d) and, with ``out`` given, out = LayerNorm(xs)
-    (bf16) with its row mean / rstd: a Linear's residual add fused into the LayerNorm after it."""
-    assert x2d.dtype == torch.float32 and xs.dtype == torch.float32 and r2d.dtype == torch.bfloat16
+    """xs = x2d + r2d (f32 + bf16 / f32 -> f32; xs may be x2d) and, with ``out`` given, out =
+    LayerNorm(xs) (bf16 / f32) with its row mean / rstd: a Linear's residual add fused into the
+    LayerNorm after it."""
+    assert x2d.dtype == torch.float32 and xs.dtype == torch.float32
     rows, D = xs.shape
     if out is not None:
-        assert out.dtype == torch.bfloat16 and mean is not None and rstd is not None
-    call("vit_add_layer_norm_fwd", rows, D, ptr(x2d), x2d.stride(0), ptr(r2d), r2d.stride(0), ptr(xs), xs.stride(0),
+        assert mean is not None and rstd is not None
+    call("vit_add_layer_norm_fwd", L.dt(r2d), L.dt(out) if out is not None else L.dt(r2d), rows, D, ptr(x2d),
+         x2d.stride(0), ptr(r2d), r2d.stride(0), ptr(xs), xs.stride(0),
          ptr(out), out.stride(0) if out is not None else 0, ptr(w), ptr(b), ptr(mean), ptr(rstd), float(eps), _s(xs))
     return xs
 
