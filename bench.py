@@ -163,14 +163,22 @@ def _block_flops(tokens, width, seq):
 
 
 def c3_step_flop(batch):
-    """Analytic FLOPs of one C3 step: the visual tower forward (24 blocks + patch embedding), the
-    last text block forward (66 prompts x 77 tokens; blocks 0-10 are a cached frozen prefix), and
-    the backward through the two DoRA visual blocks and the DoRA text block (input gradients 2x,
-    DoRA weight gradients 1x their forward GEMM FLOPs)."""
-    vis = _block_flops(batch * 257, 1024, 257)
-    txt = _block_flops(66 * 77, 768, 77)
+    """Analytic FLOPs of one C3 step, counting exactly the GEMM / attention work the kernels do
+    (DESIGN.md §4.6b).  Forward: the visual tower (24 blocks + patch embedding) and the last text
+    block (66 prompts x 77 tokens; blocks 0-10 are a cached frozen prefix).  Backward, as
+    ``_BlockFn.backward`` runs it under ``needs_input_grad`` (clip.py module docstring):
+      * visual block 23 (its input feeds block 22's DoRA gradient): fc2 and fc1 input gradients
+        (8 + 8 TD^2), out_proj weight and input gradients (2 + 2), attention backward (dP, dV, dQ,
+        dK: 8 TND; the kernels' recompute of S is not counted), qkv input gradient (6) = 26 TD^2;
+      * visual block 22 and text block 11 (nothing upstream trains): fc2, fc1 input gradients and
+        the DoRA out_proj weight gradient only = 18 TD^2.
+    LayerNorm / DoRA-weight / head backward work is not GEMM work and is left out."""
+    T, D, N = batch * 257, 1024, 257
+    Tt, Dt = 66 * 77, 768
+    vis = _block_flops(T, D, N)
+    txt = _block_flops(Tt, Dt, 77)
     fwd = 24 * vis + 2 * batch * 256 * 588 * 1024 + txt
-    bwd = 2 * (2 * vis) + 2 * txt
+    bwd = 26 * T * D * D + 8 * T * N * D + 18 * T * D * D + 18 * Tt * Dt * Dt
     return fwd + bwd
 
 

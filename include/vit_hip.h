@@ -47,6 +47,11 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
 /* Tuning hook: force GEMM tile configuration v (see csrc/gemm.hip big::V*), -1 = per-shape choice. */
 int vit_gemm_variant(int v);
 
+/* Host-only query (no GPU call): rows per launch the bf16 MFMA path uses for a row-contiguous
+ * operand of M rows x ld elements (its staging offsets are 32-bit: larger operands are split
+ * into row chunks, a multiple of 256 rows each); M when one launch fits, 0 if none does. */
+int vit_gemm_rc_chunk_rows(int M, int64_t ld);
+
 /* F.linear forward, Y = X W^T + b with fused epilogue (timm Attention.qkv/proj,
  * Mlp.fc1+GELU / fc2 + residual, head; under VIT:138-139 autocast). */
 int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const void* X, int64_t ldx,
@@ -165,10 +170,12 @@ int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, 
                         const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
                         float* sdDnT_ws, const float* noise, void* stream);
 /* torch.optim.AdamW step (NEWP:1181, NEWP:1001): tensors {float* p; const float* g; float* exp_avg;
- * float* exp_avg_sq; bf16* shadow (or null); int64 n; float step_size; float bc2_sqrt}[] where
- * step_size = lr / (1 - beta1^step) and bc2_sqrt = sqrt(1 - beta2^step) for that tensor's own
- * state['step'] (so a load_state_dict resume, NEWP:1189-1195, continues the bias correction);
- * chunks as vit_sgd_step; decay = 1 - lr * weight_decay. */
+ * float* exp_avg_sq; bf16* shadow (or null); int64 n; const float* coef}[] where coef points at
+ * the tensor's {step_size, bc2_sqrt} in device memory: step_size = lr / (1 - beta1^step) and
+ * bc2_sqrt = sqrt(1 - beta2^step) for that tensor's own state['step'] (so a load_state_dict
+ * resume, NEWP:1189-1195, continues the bias correction).  The table is fixed across steps (only
+ * the coefficients change), so a captured graph can replay it; chunks as vit_sgd_step;
+ * decay = 1 - lr * weight_decay. */
 int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, float decay, float beta1, float beta2,
                    float eps, void* stream);
 int vit_adamw_tensor_bytes(void);

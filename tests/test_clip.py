@@ -305,3 +305,68 @@ def test_c5_sweep_launcher_fp8_on_cliphba(tmp_path):
         with open(path) as fh:
             rows = [r.split(",") for r in fh.read().splitlines()[1:]]
         assert [int(r[0]) for r in rows] == list(range(e, 5)) and all(np.isfinite(float(r[2])) for r in rows)
+
+
+# ---------------------------------------------------------------------------- config C3 at the bench's shape
+
+C3_IMAGES = (0, 1, 31, 32, 63)  # straddle the f32 GEMM's 128-row tiles (64 x 257 = 16 448 rows = 128.5 tiles)
+
+
+@pytest.mark.gpu
+def test_c3_bench_shape_matches_oracle():
+    """bench.py's ``c3`` leg configuration (NEWP:274 fp32, NEWP:986-1001 step): CLIPHBA ViT-L/14 +
+    DoRA r=32 on the last 2 visual blocks and the last text block, f32, bs=64, frozen-text cache on.
+    (a) per-image predictions of images {0, 1, 31, 32, 63} against the oracle run on those five
+    images alone (the forward is per-image independent; the rows straddle the ragged 128-row f32
+    GEMM tiles); (b) the MSE loss and the 9 DoRA gradients of the bs=64 step against the oracle's
+    CPU step on the same batch.  Tolerance 1e-3 relative (north_star), max-abs over each row /
+    tensor.  Weights: oracle init_params(CLIP_L14) loaded into the product model; DoRA A/B as the
+    product's own init drew them, copied into the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import vit_amd
+    from vit_amd import clip
+    cfg, B = CR.CLIP_L14, 64
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    p = CR.init_params(cfg, seed=5)
+    prompts = CR.synthetic_prompts(66, cfg, seed=6)
+    cm = clip.build_model(p, compute_dtype=torch.float32)
+    assert cm.cache_frozen_text
+    m = vit_amd.CLIPHBA([f"c{i}" for i in range(66)], "ViT-L/14", pos_embedding=True, clip_model=cm,
+                        tokenized_prompts=prompts)
+    vit_amd.apply_dora_to_ViT(m, n_vision_layers=2, n_transformer_layers=1, r=32)
+    vit_amd.switch_dora_layers(m, freeze_all=True, dora_state=True)
+    sd = m.state_dict()
+    d = CR.init_dora(p, cfg, r=32, seed=0)
+    for k in list(d):
+        if not k.endswith(".scaling"):
+            if k.endswith(".m") or k.endswith(".D"):
+                assert _rel(sd[k], d[k]) < 1e-6, k  # DoRALayer.__init__ (NEWP:416-425) agrees
+            d[k] = sd[k].detach().clone().float()
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(B, 3, 224, 224, generator=g)
+    y = torch.randn(B, 66, generator=g) * 0.5 + 1.0
+
+    m = m.cuda()
+    with torch.no_grad():  # fills the frozen-text cache (bench warm-up does the same)
+        m(x[:2].cuda())
+    opt = vit_amd.FusedAdamW([q for q in m.parameters() if q.requires_grad], lr=3e-4)
+    opt.zero_grad(set_to_none=True)
+    pred = m(x.cuda())
+    loss = vit_amd.mse_loss(pred, y.cuda())
+    loss.backward()
+    grads = {n: q.grad.detach().cpu().clone() for n, q in m.named_parameters() if q.requires_grad}
+    torch.cuda.synchronize()
+    pred = pred.detach().cpu()
+    assert len(grads) == 9
+
+    with torch.no_grad():
+        idx = list(C3_IMAGES)
+        pr5 = CR.forward(p, x[idx], prompts, cfg, d, pos_embedding=True)
+    for r, i in enumerate(idx):
+        assert _rel(pred[i], pr5[r]) < 1e-3, (i, _rel(pred[i], pr5[r]))
+    ref_loss, ref_pred, ref_grads = CR.train_step(p, d, {}, x, prompts, y, cfg, lr=3e-4, pos_embedding=True)
+    assert _rel(pred, ref_pred) < 1e-3
+    assert abs(float(loss.detach()) - ref_loss) <= 1e-3 * abs(ref_loss)
+    for k, rg in ref_grads.items():
+        assert _rel(grads[k], rg) < 1e-3, (k, _rel(grads[k], rg))

@@ -121,6 +121,36 @@ def test_linear_dgrad_fused_bias(M, N, K, dtype):
     _close(db, ref.sum(0), 1e-5, "dbias")
 
 
+def test_gemm_rc_operand_past_4gib_is_chunked():
+    """An RC operand whose staging offsets pass 2^32 bytes (a [M, 1024]-strided bf16 view over
+    4.3 GB) runs as row chunks with every row-indexed operand shifted: forward and
+    GELU' dgrad with fused bias sums, checked around the chunk seam and in total."""
+    M, LD, K, N = (1 << 21) + 768, 1024, 64, 256
+    assert L.lib().vit_gemm_rc_chunk_rows(M, LD) == 1 << 21
+    g = torch.Generator(device=DEV).manual_seed(3)
+    buf = torch.randn(M, LD, device=DEV, generator=g).to(torch.bfloat16)
+    x = buf[:, :K]
+    w = (torch.randn(N, K, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    b = torch.randn(N, device=DEV, generator=g)
+    y = ops.linear_fwd(x, w, b, out_dtype=torch.bfloat16)
+    for r0, r1 in ((0, 512), ((1 << 21) - 512, (1 << 21) + 512), (M - 300, M)):
+        ref = x[r0:r1].float() @ w.float().T + b
+        _close(y[r0:r1], ref, 8e-3, f"fwd rows {r0}:{r1}")
+    del y
+    wd = (torch.randn(K, N, device=DEV, generator=g) * 0.1).to(torch.bfloat16)  # dX[M, N] = dY[M, K] W[K, N]
+    pre = torch.randn(M, N, device=DEV, generator=g).to(torch.bfloat16)
+    db = torch.empty(N, device=DEV)
+    d = ops.linear_dgrad(x, wd, out_dtype=torch.bfloat16, epi=L.EPI_GELU_BWD, pre=pre, dbias=db)
+    ref_sum = torch.zeros(N, device=DEV, dtype=torch.float64)
+    for r0 in range(0, M, 1 << 19):
+        r1 = min(M, r0 + (1 << 19))
+        ref = (x[r0:r1].float() @ wd.float()) * pre[r0:r1].float()
+        if r0 <= (1 << 21) < r1 or r1 == M:
+            _close(d[r0:r1], ref, 8e-3, f"gelu' dgrad rows {r0}:{r1}")
+        ref_sum += ref.double().sum(0)
+    _close(db, ref_sum.float(), 1e-3, "fused bias sums across chunks")
+
+
 @pytest.mark.parametrize("M,N,K,split", [(1024, 256, 384, 1), (4096, 384, 256, 4), (6336, 256, 128, 7), (6304, 256, 128, 3)])
 def test_linear_wgrad(M, N, K, split):
     dy = _rnd(M, N, seed=11, dtype=torch.bfloat16)
@@ -322,7 +352,7 @@ def test_layer_norm_fwd_bwd(D, xdt):
     _close(db, br.grad, 1e-5, "dbeta")
 
 
-@pytest.mark.parametrize("D", [768, 1024])
+@pytest.mark.parametrize("D", [768, 1024, 1280, 1792])
 def test_add_layer_norm_fwd(D):
     """xs = x + r (f32 + bf16), y = LayerNorm(xs) in bf16, mean/rstd; in place (xs is x) and add-only."""
     M = 333
@@ -549,6 +579,52 @@ def test_fused_adamw_matches_torch():
         opt.step()
     for p, q in zip(ps, qs):
         _close(q, p, 1e-6, "adamw")
+
+
+def test_fused_adamw_table_is_static_and_graph_replay_matches_torch():
+    """The AdamW tensor table holds pointers and sizes only (its key does not change from step to
+    step: ADVICE r02); a captured step() replayed after prepare_replay() follows torch.AdamW."""
+    from vit_amd.optim import FusedAdamW
+    torch.manual_seed(3)
+    shapes = [(48, 512), (512,), (3,)]
+    ps = [torch.nn.Parameter(torch.randn(s)) for s in shapes]
+    qs = [torch.nn.Parameter(p.detach().clone().to(DEV)) for p in ps]
+    gdev = [torch.zeros(s, device=DEV) for s in shapes]
+    for q, g in zip(qs, gdev):
+        q.grad = g
+    ref = torch.optim.AdamW(ps, lr=3e-4, weight_decay=0.01)
+    opt = FusedAdamW(qs, lr=3e-4, weight_decay=0.01)
+    grads = [[torch.randn(s) for s in shapes] for _ in range(6)]
+
+    def feed(gs):
+        for p, g, gd in zip(ps, gs, gdev):
+            p.grad = g.clone()
+            gd.copy_(g)
+
+    feed(grads[0])
+    ref.step()
+    opt.step()  # eager: builds the table
+    key = opt._mt[0]._key
+    feed(grads[1])
+    ref.step()
+    opt.step()
+    assert opt._mt[0]._key == key  # same table on the next step
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            opt.step()
+    torch.cuda.current_stream().wait_stream(s)
+    for gs in grads[2:]:
+        feed(gs)
+        ref.step()
+        opt.prepare_replay()
+        graph.replay()
+    torch.cuda.synchronize()
+    for p, q in zip(ps, qs):
+        _close(q, p, 1e-6, "adamw graph replay")
+    assert all(float(opt.state[q]["step"]) == 6.0 for q in qs)
 
 
 def test_fused_adamw_resume_continues_bias_correction():

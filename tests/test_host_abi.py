@@ -28,9 +28,30 @@ def test_library_exports_every_header_symbol():
         assert name in _lib.SIGNATURES, f"{name} missing from the ctypes signature table"
     for name in _lib.SIGNATURES:
         assert name in declared, f"{name} bound in Python but not declared in include/vit_hip.h"
-    assert lib.vit_abi_version() == 4
+    assert lib.vit_abi_version() == 5
     assert lib.vit_sgd_tensor_bytes() == 40 and lib.vit_sgd_chunk_bytes() == 16
     assert lib.vit_sgd_chunk_size() == 4096
+
+
+def test_gemm_32bit_offset_plan():
+    """The bf16 MFMA GEMM stages row-contiguous operands through 32-bit byte offsets (gemm.hip
+    gemm_tile): operands past 4 GiB are split into row chunks (multiples of 256 rows) so the
+    offsets never wrap.  Host-only query, no GPU call."""
+    from vit_amd import _lib
+    lib = _lib.load()
+    rows = lib.vit_gemm_rc_chunk_rows
+    M = 256 * 197
+    assert rows(M, 3072) == M and rows(M, 768) == M  # the bench shapes: one launch
+    for m, ld in ((3600 * 197, 3072), (2100 * 257, 4096), (1 << 21, 1024), (5000 * 197, 768)):
+        r = rows(m, ld)
+        fits = (m - 1) * ld * 2 + 128 < (1 << 32)
+        if fits:
+            assert r == m
+        else:
+            assert 0 < r < m and r % 256 == 0, (m, ld, r)
+            assert (r - 1) * ld * 2 + 128 < (1 << 32) <= (r + 255) * ld * 2 + 128, (m, ld, r)
+    assert rows(3600 * 197, 3072) < 3600 * 197  # fc1 activations at bs 3600 (ADVICE example)
+    assert rows(1000, 1 << 25) == 0  # 64 MiB rows: no 256-row chunk fits, the fast path is refused
 
 
 def test_library_is_gfx950_code_object(tmp_path):

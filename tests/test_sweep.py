@@ -4,6 +4,7 @@ early stopping), exercised on CPU with a stand-in model that has the DoRA parame
 the reference's module paths (the real CLIPHBA needs the GPU kernels: tests/test_clip.py)."""
 import csv
 import os
+import random
 import sys
 
 import numpy as np
@@ -105,7 +106,8 @@ def test_dora_and_random_state_files_match_reference_format(tmp_path):
     g = torch.Generator().manual_seed(7)
     rf = S.save_random_states(opt, 4, str(tmp_path / "rs"), g)
     assert os.path.basename(rf) == "epoch5_random_states.pth"
-    ck = torch.load(rf, weights_only=False)
+    with torch.serialization.safe_globals(S._rng_state_globals()):
+        ck = torch.load(rf, weights_only=True)
     assert {'epoch', 'optimizer_state_dict', 'torch_rng_state', 'numpy_rng_state', 'python_rng_state',
             'dataloader_generator_state'} <= set(ck)
     a = torch.rand(3)
@@ -114,6 +116,30 @@ def test_dora_and_random_state_files_match_reference_format(tmp_path):
     assert torch.equal(torch.rand(3), a)  # torch RNG restored to the saved point
     assert torch.equal(g2.get_state(), ck['dataloader_generator_state'])
     assert not S.load_random_states(str(tmp_path / "rs"), 99)
+
+
+class _Payload:
+    """A pickled object whose reconstruction would run code (os.system here)."""
+
+    def __reduce__(self):
+        return (os.system, ("echo pwned > /dev/null",))
+
+
+def test_load_random_states_refuses_non_allowlisted_globals(tmp_path):
+    import pickle
+    d = tmp_path / "rs"
+    d.mkdir()
+    ck = {'epoch': 3, 'torch_rng_state': torch.get_rng_state(), 'numpy_rng_state': np.random.get_state(),
+          'python_rng_state': random.getstate(), 'evil': _Payload()}
+    torch.save(ck, str(d / "epoch4_random_states.pth"))
+    before = torch.get_rng_state()
+    with pytest.raises(pickle.UnpicklingError):
+        S.load_random_states(str(d), 4)
+    assert torch.equal(torch.get_rng_state(), before)  # nothing was applied
+    # the same file without the payload resumes
+    del ck['evil']
+    torch.save(ck, str(d / "epoch4_random_states.pth"))
+    assert S.load_random_states(str(d), 4)
 
 
 def test_train_condition_window_csv_and_resume(tmp_path):

@@ -101,9 +101,11 @@ __global__ __launch_bounds__(256) void dora_bwd_row_kernel(int in, int out, cons
 // step_size = lr / (1 - b1^step) and sqrt(1 - b2^step) are computed per tensor in
 // double on the host from that tensor's own state['step'] (as torch does), so a
 // resumed optimizer (load_state_dict) continues the bias correction where it was.
-// The bf16 GEMM shadow of the parameter (if any) is written in the same pass.
+// They live in a separate device array (coef = {step_size, bc2_sqrt} of this tensor)
+// refreshed by one copy per step, so the tensor table itself never changes between
+// steps.  The bf16 GEMM shadow of the parameter (if any) is written in the same pass.
 // ---------------------------------------------------------------------------
-struct AdamTensor { float* p; const float* g; float* m; float* v; bf16* shadow; int64_t n; float step_size; float bc2_sqrt; };
+struct AdamTensor { float* p; const float* g; float* m; float* v; bf16* shadow; int64_t n; const float* coef; };
 struct AdamChunk { int tensor; int pad; int64_t start; };
 constexpr int ADAM_CHUNK = 4096;
 
@@ -113,14 +115,15 @@ __global__ __launch_bounds__(256) void adamw_kernel(const AdamTensor* __restrict
   const AdamTensor t = ts[ch.tensor];
   const float w1 = 1.f - b1, w2 = 1.f - b2;
   const int64_t end = min(t.n, ch.start + ADAM_CHUNK);
+  const float step_size = t.coef[0], bc2_sqrt = t.coef[1];
   for (int64_t i = ch.start + threadIdx.x; i < end; i += 256) {
     float p = __fmul_rn(t.p[i], decay);
     const float g = t.g[i];
     float m = t.m[i];
     m = __fadd_rn(m, __fmul_rn(w1, __fsub_rn(g, m)));  // torch lerp, weight < 0.5 branch
     float v = __fadd_rn(__fmul_rn(t.v[i], b2), __fmul_rn(__fmul_rn(w2, g), g));
-    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), t.bc2_sqrt), eps);
-    p = __fsub_rn(p, __fmul_rn(t.step_size, __fdiv_rn(m, denom)));
+    const float denom = __fadd_rn(__fdiv_rn(__fsqrt_rn(v), bc2_sqrt), eps);
+    p = __fsub_rn(p, __fmul_rn(step_size, __fdiv_rn(m, denom)));
     t.p[i] = p; t.m[i] = m; t.v[i] = v;
     if (t.shadow) t.shadow[i] = (bf16)p;
   }
@@ -162,7 +165,7 @@ int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, 
                   stream);
 }
 
-// Fused AdamW over a table of AdamTensor {p, g, m, v, shadow, n, step_size, bc2_sqrt};
+// Fused AdamW over a table of AdamTensor {p, g, m, v, shadow, n, coef -> {step_size, bc2_sqrt}};
 // chunks of 4096 elements {tensor, pad, start}; decay = 1 - lr * weight_decay.
 int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, float decay, float beta1, float beta2,
                    float eps, void* stream) {

@@ -1099,9 +1099,26 @@ __global__ void colsum_partial_kernel(const T* __restrict__ X, int64_t ld, int M
 // edge, the epilogue guards i < M: e.g. the 66 x 77 = 5082 text-tower tokens);
 // an i/j-contiguous (CR) one loads 8-wide column chunks, so it needs a multiple
 // of 8; the 4-column epilogue stores need N % 4.
+// big::gemm_tile addresses an RC operand through per-lane uint32 byte offsets from a k-advanced
+// base: the largest one is (rows - 1) * ld * 2 plus a 64-element (128-B) chunk.  Larger operands
+// are split along the rows by the dispatcher (rc_chunk_rows); the CR layouts keep offsets below
+// BK rows and need no limit.
+static constexpr int64_t kOffLimit = (int64_t)1 << 32;
+static bool rc_offsets_fit(int rows, int64_t ld) { return (int64_t)(rows > 0 ? rows - 1 : 0) * ld * 2 + 128 < kOffLimit; }
+// rows per launch for an RC operand of `ld` elements per row: a multiple of 256 (the largest BM, and
+// of 64 for the column-sum partial rows) whose offsets fit; M itself when it fits
+static int rc_chunk_rows(int M, int64_t ld) {
+  if (rc_offsets_fit(M, ld)) return M;
+  const int64_t r = ((kOffLimit - 129) / (ld * 2) + 1) / 256 * 256;  // the most rows that fit, in 256s
+  return (int)(r > 0 ? r : 0);
+}
+
 static bool fast_ok(int dtype, int pl, int ql, int M, int N, int R, const void* P, const void* Q, int64_t ldp,
                     int64_t ldq) {
   if (dtype != VIT_BF16) return false;
+  // an RC Q (the weights of a forward GEMM) must fit the 32-bit offsets whole; an RC P is chunked
+  if (ql == LAY_RC && !rc_offsets_fit(N, ldq)) return false;
+  if (pl == LAY_RC && rc_chunk_rows(M, ldp) == 0) return false;
   if ((pl == LAY_CR && M % 8) || (ql == LAY_CR && N % 8) || N % 4 || R % 32 || R <= 0) return false;
   if ((ldp % 8) || (ldq % 8)) return false;
   if (((uintptr_t)P & 15) || ((uintptr_t)Q & 15)) return false;
@@ -1317,6 +1334,31 @@ static int gemm_dispatch(int dtype, int out_dtype, int pl, int ql, int M, int N,
                          const void* P, int64_t ldp, const void* Q, int64_t ldq, int split,
                          const Epi& e, hipStream_t s, bool allow_fast) {
   if (M <= 0 || N <= 0) return 0;
+  if (allow_fast && fast_ok(dtype, pl, ql, M, N, R, P, Q, ldp, ldq) && (e.ldc % 4 == 0) && pl == LAY_RC) {
+    // an RC P past the 32-bit staging offsets: launch row chunks with every row-indexed operand
+    // shifted (the patch epilogue's row remap and split slabs are not row-shiftable: generic path)
+    const int rows = rc_chunk_rows(M, ldp);
+    if (rows < M) {
+      if (EPI == EPI_PATCH || split > 1) {
+        allow_fast = false;
+      } else {
+        const size_t osz = out_dtype == VIT_F32 ? 4 : 2;
+        const size_t asz = (EPI == EPI_RESID) ? 4 : 2;  // RESID: f32 stream; *_BWD: pre-activation (bf16 here)
+        for (int r0 = 0; r0 < M; r0 += rows) {
+          const int m = M - r0 < rows ? M - r0 : rows;
+          Epi c = e;
+          c.C = (char*)e.C + (size_t)r0 * e.ldc * osz;
+          if (e.aux) c.aux = (const char*)e.aux + (size_t)r0 * e.ld_aux * asz;
+          if (e.aux_out) c.aux_out = (char*)e.aux_out + (size_t)r0 * e.ldc * osz;
+          if (e.csum) c.csum = e.csum + (int64_t)(r0 / 64) * N;
+          const int rc = gemm_dispatch<EPI>(dtype, out_dtype, pl, ql, m, N, R, (const char*)P + (size_t)r0 * ldp * 2,
+                                            ldp, Q, ldq, split, c, s, true);
+          if (rc) return rc;
+        }
+        return 0;
+      }
+    }
+  }
   if (allow_fast && fast_ok(dtype, pl, ql, M, N, R, P, Q, ldp, ldq) && (e.ldc % 4 == 0)) {
 #define FAST(PLx, QLx)                                                                                  \
     if (out_dtype == VIT_F32) {                                                                         \
@@ -1366,6 +1408,11 @@ static int gemm_any(int epi, int dtype, int out_dtype, int pl, int ql, int M, in
 static Epi make_epi() { Epi e; memset(&e, 0, sizeof(e)); e.dbg = g_dbg; return e; }
 
 extern "C" {
+
+// Host-side plan of the bf16 MFMA path's 32-bit staging offsets (no GPU needed; tests):
+// rows per launch for an RC operand of M rows and `ld` elements per row (M when it fits one
+// launch, 0 when even 256 rows do not fit).
+int vit_gemm_rc_chunk_rows(int M, int64_t ld) { return rc_chunk_rows(M, ld); }
 
 // Tuning hook: force GEMM configuration big::V<v> (-1 restores the per-shape heuristic).
 int vit_gemm_variant(int v) { g_variant = v; g_dbg = v >= 100 ? v / 100 : 0; return 0; }

@@ -347,7 +347,9 @@ int vit_add_layer_norm_fwd(int dtype_r, int dtype_y, int rows, int D, const floa
     case 2: AD(2) break;
     case 3: AD(3) break;
     case 4: AD(4) break;
+    case 5: AD(5) break;
     case 6: AD(6) break;
+    case 7: AD(7) break;
     case 8: AD(8) break;
     default: return (int)hipErrorInvalidValue;
   }

@@ -26,6 +26,7 @@ i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
 SIGNATURES = {
     "vit_abi_version": [],
     "vit_gemm_variant": [i32],
+    "vit_gemm_rc_chunk_rows": [i32, i64],
     "vit_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, vp],
     "vit_linear_fwd": [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, i64, vp, vp, vp],
     "vit_linear_dgrad": [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, i64, vp, vp, vp, i64, i32, vp],

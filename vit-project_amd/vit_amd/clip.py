@@ -333,7 +333,7 @@ class CLIP(nn.Module):
         first = _first_trainable(blocks)
         # the residual adds run inside the next LayerNorm (as the ViT blocks, model._tokens); in f32 the
         # same f32 add as the GEMM's residual epilogue, so the reference-precision result is unchanged
-        rs = ({"pending": None} if (_FUSED_RESID[0] and (T != torch.float32 or _FUSED_RESID_F32[0]) and W % 256 == 0)
+        rs = ({"pending": None} if (_FUSED_RESID[0] and (T != torch.float32 or _FUSED_RESID_F32[0]) and ops.add_layer_norm_supported(W))
               else None)
         for i, blk in enumerate(blocks):
             cfg = self._cfg(heads, False, frozen=i < first)

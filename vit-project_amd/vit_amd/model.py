@@ -190,19 +190,23 @@ def cfg_defer_bwd(ctx) -> bool:
     return getattr(ctx, "defer_bwd", False)
 
 
-_JOIN_QUEUED = set()
+_JOIN_QUEUED = set()  # (graph task id, device) pairs whose end-of-backward join is queued
 
 
 def _queue_backward_join(dev):
     """Deferred-join backward: make sure the side stream is joined when this backward pass
     ends, even if the patch embedding's backward (the normal join point) never runs --
-    ``backward(inputs=...)`` / ``autograd.grad`` that stop above it."""
-    if dev in _JOIN_QUEUED:
+    ``backward(inputs=...)`` / ``autograd.grad`` that stop above it.  The dedup key is the
+    current autograd graph task, so a backward that raised (its final callbacks never run) does
+    not suppress the join of the next one."""
+    key = (torch._C._current_graph_task_id(), dev)
+    if key in _JOIN_QUEUED:
         return
-    _JOIN_QUEUED.add(dev)
+    _JOIN_QUEUED.clear()  # entries of earlier graph tasks are finished (or abandoned)
+    _JOIN_QUEUED.add(key)
 
     def _join():
-        _JOIN_QUEUED.discard(dev)
+        _JOIN_QUEUED.discard(key)
         _Side(dev).join()
 
     torch.autograd.Variable._execution_engine.queue_callback(_join)
@@ -726,7 +730,7 @@ class VisionTransformer(nn.Module):
         # fp8 attention (set_attention_fp8): forward passes that build no graph (eval / RSA)
         cfg["attn_fp8"] = self._attn_fp8 and not torch.is_grad_enabled()
         D = self.embed_dim
-        if _FUSED_RESID[0] and (self.compute_dtype != torch.float32 or _FUSED_RESID_F32[0]) and D % 256 == 0:
+        if _FUSED_RESID[0] and (self.compute_dtype != torch.float32 or _FUSED_RESID_F32[0]) and ops.add_layer_norm_supported(D):
             cfg["resid"] = {"pending": None}  # residual adds inside the LayerNorms (_BlockFn.forward)
         for i, blk in enumerate(self.blocks):
             bcfg = cfg if i != 0 else dict(cfg, compact_np=pe.num_patches)

@@ -189,6 +189,12 @@ def layer_norm_fwd(x2d, w, b, eps, out_dtype, rows=None, ldx=None, out=None, nee
     return out, mean, rstd
 
 
+def add_layer_norm_supported(D: int) -> bool:
+    """Widths ``vit_add_layer_norm_fwd`` takes: D a multiple of 256 up to 2048 (ViT-B 768, ViT-L
+    1024, ViT-H 1280, ...); other widths keep the residual add in the GEMM epilogue."""
+    return D % 256 == 0 and 256 <= D <= 2048
+
+
 def add_layer_norm_fwd(x2d, r2d, xs, w=None, b=None, eps=1e-6, out=None, mean=None, rstd=None):
     """xs = x2d + r2d (f32 + bf16 / f32 -> f32; xs may be x2d) and, with ``out`` given, out =
     LayerNorm(xs) (bf16 / f32) with its row mean / rstd: a Linear's residual add fused into the

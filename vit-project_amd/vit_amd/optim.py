@@ -7,7 +7,8 @@ makes the first step identical to torch's ``buf = d.clone()``), writing the bf16
 GEMM shadow of each weight in the same pass.  ``lr`` lives in a device scalar so
 a captured HIP graph follows the schedule (call :meth:`sync_lr` outside the graph).
 
-``FusedAdamW`` is ``torch.optim.AdamW`` (NEWP:1181; amsgrad off) the same way.
+``FusedAdamW`` is ``torch.optim.AdamW`` (NEWP:1181; amsgrad off) the same way; its per-step
+bias corrections travel in a separate device array, so its tensor table is fixed too.
 ``CosineAnnealingLRWithWarmup`` restates VIT:206-244 (stepped once per epoch
 after training, so epoch 0 runs at the base LR: quirk Q1).
 """
@@ -147,11 +148,6 @@ class FusedSGD(torch.optim.Optimizer):
         return loss
 
 
-def _f32_pair(a: float, b: float) -> int:
-    """Two float32 values packed little-endian into one int64 table slot."""
-    return int(np.array([a, b], dtype=np.float32).view(np.int64)[0])
-
-
 def _mark_updated(p: torch.Tensor):
     """A parameter was rewritten through a raw pointer: bump its version counter (what an
     in-place torch op would do), so version-keyed caches (the bf16 GEMM shadow, the CLIP
@@ -168,12 +164,73 @@ class FusedAdamW(torch.optim.Optimizer):
     ``exp_avg_sq``), so ``state_dict()`` / ``load_state_dict()`` round-trip with
     ``torch.optim.AdamW`` and a resumed optimizer (NEWP:1189-1195) continues each tensor's
     bias correction from its saved ``step``.  Bias corrections are computed in double on the
-    host per tensor, as torch's single-tensor path does; the kernel also refreshes the bf16
-    GEMM shadow of shadowed weights."""
+    host per tensor, as torch's single-tensor path does, into a small device array (one
+    host-to-device copy per step from a pinned ring); the tensor table the kernel reads holds
+    only pointers and sizes, so it is built once and stays fixed.  The kernel also refreshes
+    the bf16 GEMM shadow of shadowed weights.
+
+    HIP-graph capture: after one eager step (which builds the table), ``step()`` under capture
+    records the update kernel only; call :meth:`prepare_replay` outside the graph before each
+    replay -- it advances every ``state['step']`` and uploads that step's coefficients."""
+
+    RING = 4  # pinned coefficient buffers in flight (the host waits only when it is RING steps ahead)
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._mt = {}
+        self._coef = {}   # group index -> device float32 [2 * ntensors]
+        self._ring = {}   # group index -> [pinned host buffer, event or None] * RING
+        self._ring_pos = {}
+        self._captured = {}  # group index -> the parameter list a capture recorded
+
+    def _group_params(self, group):
+        return [p for p in group["params"] if p.grad is not None]
+
+    def _advance(self, group, params):
+        """state['step'] += 1 for each tensor; the (lr / bc1, sqrt(bc2)) pairs of the new step."""
+        lr, (b1, b2) = float(group["lr"]), group["betas"]
+        coef = np.empty(2 * len(params), dtype=np.float32)
+        for i, p in enumerate(params):
+            st = self.state[p]
+            if len(st) == 0:
+                st["step"] = torch.tensor(0.0, dtype=torch.float32)
+                st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            st["step"] += 1
+            step = float(st["step"].item())
+            coef[2 * i] = lr / (1.0 - b1 ** step)
+            coef[2 * i + 1] = math.sqrt(1.0 - b2 ** step)
+        return coef
+
+    def _upload(self, gi, coef, dev):
+        """One async copy of this step's coefficients into the group's device array, through a
+        ring of pinned buffers (a buffer is rewritten only after its previous copy finished)."""
+        cd = self._coef.get(gi)
+        if cd is None or cd.numel() != coef.size or cd.device != dev:
+            cd = self._coef[gi] = torch.empty(coef.size, dtype=torch.float32, device=dev)
+            self._ring[gi] = [[torch.empty(coef.size, dtype=torch.float32).pin_memory(), None]
+                              for _ in range(self.RING)]
+            self._ring_pos[gi] = 0
+        k = self._ring_pos[gi]
+        slot = self._ring[gi][k]
+        if slot[1] is not None:
+            slot[1].synchronize()
+        slot[0].numpy()[:] = coef
+        cd.copy_(slot[0], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        slot[1] = ev
+        self._ring_pos[gi] = (k + 1) % self.RING
+        return cd
+
+    @torch.no_grad()
+    def prepare_replay(self):
+        """Before each replay of a graph that captured ``step()``: advance the steps and upload
+        the coefficients the captured kernel will read (eager mode never needs this)."""
+        for gi, group in enumerate(self.param_groups):
+            params = self._captured.get(gi)
+            if params:
+                self._upload(gi, self._advance(group, params), params[0].device)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -181,32 +238,38 @@ class FusedAdamW(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        capturing = torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
         for gi, group in enumerate(self.param_groups):
-            params = [p for p in group["params"] if p.grad is not None]
+            params = self._group_params(group)
             if not params:
                 continue
             dev = params[0].device
             L.require_gpu(torch.empty(0, device=dev))
             lr, (b1, b2), eps, wd = float(group["lr"]), group["betas"], float(group["eps"]), float(group["weight_decay"])
+            if capturing:
+                if self._coef.get(gi) is None:
+                    raise RuntimeError("FusedAdamW: run one eager step() before capturing (it builds the tensor "
+                                       "table and the coefficient buffer); then call prepare_replay() before "
+                                       "each replay")
+                self._captured[gi] = params
+                cd = self._coef[gi]
+            else:
+                coef = self._advance(group, params)
+                for p in params:
+                    st = self.state[p]
+                    if not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
+                        p.grad = p.grad.float().contiguous()
+                    for k in ("exp_avg", "exp_avg_sq"):
+                        if st[k].device != p.device or not st[k].is_contiguous():
+                            st[k] = st[k].to(p.device).contiguous()
+                cd = self._upload(gi, coef, dev)
             entries, sizes = [], []
-            for p in params:
+            base = cd.data_ptr()
+            for i, p in enumerate(params):
                 st = self.state[p]
-                if len(st) == 0:
-                    st["step"] = torch.tensor(0.0, dtype=torch.float32)
-                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                st["step"] += 1
-                step = float(st["step"].item())
-                bc1 = 1.0 - b1 ** step
-                bc2 = 1.0 - b2 ** step
-                if not p.grad.is_contiguous() or p.grad.dtype != torch.float32:
-                    p.grad = p.grad.float().contiguous()
-                for k in ("exp_avg", "exp_avg_sq"):
-                    if st[k].device != p.device or not st[k].is_contiguous():
-                        st[k] = st[k].to(p.device).contiguous()
                 sh = getattr(p, "_vit_shadow", None)
                 entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                                None if sh is None else sh.data_ptr(), p.numel(), _f32_pair(lr / bc1, math.sqrt(bc2))))
+                                None if sh is None else sh.data_ptr(), p.numel(), base + 8 * i))
                 sizes.append(p.numel())
             mt = self._mt.get(gi)
             if mt is None:

@@ -19,9 +19,11 @@ new_cvpr_train_behavior_things_pipeline.py):
 
 Data is whatever the caller passes as (images, targets) tensors -- THINGS images and SPOSE
 targets are not in the reference tree; the driver's tests use synthetic ones.  The RNG-state
-files are pickles holding numpy / Python RNG tuples, exactly as the reference writes them:
-``load_random_states`` is meant for files this runner (or the reference) wrote, and reads them
-with ``weights_only=False`` for that reason only.
+files are pickles holding numpy / Python RNG tuples, exactly as the reference writes them.
+``load_random_states`` reads them with ``torch.load(weights_only=True)`` and an allow-list of
+exactly the globals such a file needs (numpy's ndarray / dtype reconstruction, in both the
+numpy 1.x and 2.x module paths); a file naming any other global is refused, so a resume never
+executes code from the checkpoint.
 """
 from __future__ import annotations
 
@@ -97,12 +99,31 @@ def save_random_states(optimizer, epoch, random_state_path, dataloader_generator
     return f
 
 
+def _rng_state_globals():
+    """The globals a reference RNG-state file references (numpy's MT19937 state is an ndarray
+    inside a tuple): ndarray / dtype reconstruction under numpy 2.x (``numpy._core``) and 1.x
+    (``numpy.core``), plus the per-dtype classes numpy >= 1.25 pickles dtypes with."""
+    import numpy.dtypes as npd
+    g = [np.ndarray, np.dtype]
+    g += [getattr(npd, n) for n in ("UInt32DType", "Int64DType", "Float64DType") if hasattr(npd, n)]
+    for mod in ("numpy._core.multiarray", "numpy.core.multiarray"):
+        try:
+            m = __import__(mod, fromlist=["_reconstruct"])
+        except ImportError:
+            continue
+        g.append((m._reconstruct, f"{mod}._reconstruct"))
+    return g
+
+
 def load_random_states(random_state_path, epoch, optimizer=None, dataloader_generator=None) -> bool:
-    """NEWP:88-135; False when the file does not exist (the reference's behaviour)."""
+    """NEWP:88-135; False when the file does not exist (the reference's behaviour).
+    Weights-only load: the allow-list is ``_rng_state_globals``; anything else in the pickle
+    raises ``pickle.UnpicklingError`` before any of it runs."""
     f = os.path.join(random_state_path, f"epoch{epoch}_random_states.pth")
     if not os.path.exists(f):
         return False
-    ck = torch.load(f, weights_only=False)  # numpy / Python RNG tuples (see module docstring)
+    with torch.serialization.safe_globals(_rng_state_globals()):
+        ck = torch.load(f, map_location="cpu", weights_only=True)
     torch.set_rng_state(ck['torch_rng_state'])
     np.random.set_state(ck['numpy_rng_state'])
     random.setstate(ck['python_rng_state'])
