@@ -47,6 +47,11 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
 /* Tuning hook: force GEMM tile configuration v (see csrc/gemm.hip big::V*), -1 = per-shape choice. */
 int vit_gemm_variant(int v);
 
+/* Tuning hook: the forward / input-gradient GEMMs walk their tiles in bands of `fwd` / `dgrad`
+ * row tiles, column-major inside a band (L2 reuse of the weight columns); 0 = row-major, -1 = the
+ * per-shape default (bands of 8 for wide outputs with >= 4 MiB weights). */
+int vit_gemm_group(int fwd, int dgrad);
+
 /* Host-only query (no GPU call): rows per launch the bf16 MFMA path uses for a row-contiguous
  * operand of M rows x ld elements (its staging offsets are 32-bit: larger operands are split
  * into row chunks, a multiple of 256 rows each); M when one launch fits, 0 if none does. */
@@ -73,6 +78,13 @@ int vit_linear_dgrad_partial_floats(int M, int K);
  * in `workspace` (>= split*N*K*4 bytes) -- autograd of VIT:142. */
 int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t lddy, const void* X,
                      int64_t ldx, float* dW, int split, void* workspace, int64_t ws_bytes, void* stream);
+/* The same weight gradient as split-K partials only: slabs[z][N*K] f32 for
+ * z < vit_linear_wgrad_nslabs(...), dW = sum_z slabs[z] (ragged M % 32 rows folded into the last
+ * slab); the caller reduces them -- the block backward's single vit_colreduce_batch launch
+ * (S = nslabs, N = N*K).  bf16, or f32 on the MFMA path. */
+int vit_linear_wgrad_nslabs(int dtype, int M, int N, int K, int split);
+int vit_linear_wgrad_partials(int dtype, int M, int N, int K, const void* dY, int64_t lddy, const void* X,
+                              int64_t ldx, int split, float* slabs, int64_t slab_bytes, void* stream);
 
 /* Column sums (bias gradients): out[N] = sum_i X[i][:] -- autograd of VIT:142. */
 int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, float* partial,
@@ -85,6 +97,17 @@ int vit_colreduce(const float* part, int S, int N, float* out, int accumulate, f
  * (>= nq*ceil(S/64)*N floats). */
 int vit_colreduce_multi(const float* part, int nq, int S, int N, float* out0, float* out1, float* out2,
                         int accumulate, float* scratch, void* stream);
+
+/* Every deferred column reduction of one transformer block's backward (the bias gradients of
+ * qkv / proj / fc1 / fc2 and the norm1 / norm2 affine gradients, autograd of VIT:142) in ONE
+ * launch: jobs = njobs x {part, out, S, N, accumulate} as int64 in host memory, each
+ * out[N] (+)= sum of the S rows of part [S][N].  Sums run in a fixed order (bitwise reproducible);
+ * jobs with more than 64 partial rows combine 64-row chunk partials in-launch (agent-scope
+ * release/acquire + a ticket counter per 256-column strip).  scratch / counters sized by
+ * vit_colreduce_batch_sizes; counters zero-filled before first use (the kernel leaves them zero). */
+int vit_colreduce_batch_sizes(const int64_t* jobs, int njobs, int64_t* scratch_floats, int* counters);
+int vit_colreduce_batch(const int64_t* jobs, int njobs, float* scratch, int64_t scratch_floats, int* counters,
+                        int ncounters, void* stream);
 
 /* timm PatchEmbed Conv2d(3,768,16,16) as GEMM over unfolded patches, writing
  * rows b*(np+1)+1+p of the f32 token stream with pos_embed added (VIT:139). */
@@ -137,7 +160,9 @@ int vit_sdpa_fwd_fp8(int dtype, int B, int H, int N, int head_dim, const void* q
                      int64_t ld_o, float* lse, float scale, int causal, void* stream);
 /* SDPA backward into dqkv (qkv layout). delta_ws >= B*H*N floats.  dbias (optional, [3*H*64]) =
  * column sums of dqkv (the qkv Linear's bias gradient), fused into the kernels;
- * partial >= vit_sdpa_bwd_partial_floats(B, N, H*64). */
+ * partial >= vit_sdpa_bwd_partial_floats(B, N, H*64).  dbias == NULL with partial != NULL (bf16
+ * only): the kernels leave the per-image [B][3*H*64] partial sums in `partial` for the caller to
+ * reduce (vit_colreduce_batch). */
 int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, int64_t ld_qkv, const void* o,
                  int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, void* dqkv, int64_t ld_dqkv,
                  float* delta_ws, float scale, int causal, float* dbias, float* partial, int64_t partial_floats,

@@ -160,6 +160,47 @@ def test_linear_wgrad(M, N, K, split):
     _close(dw, ref, 2e-5, "wgrad")
 
 
+@pytest.mark.parametrize("M,N,K,split,dtype", [(6336, 256, 128, 7, torch.bfloat16), (6304 + 19, 256, 384, 3, torch.bfloat16),
+                                               (4096, 512, 256, 4, torch.float32), (50, 256, 128, 2, torch.bfloat16)])
+def test_linear_wgrad_partials_sum_to_dw(M, N, K, split, dtype):
+    """Split-K slabs only (vit_linear_wgrad_partials, reduced later by the block's batch launch):
+    their sum is dW, including a ragged M % 32 tail folded into the last slab; through ColBatch
+    the result agrees with the immediate path's reduction to rounding (the batch sums the slabs
+    in a different fixed order)."""
+    dy = _rnd(M, N, seed=13, dtype=dtype)
+    x = _rnd(M, K, seed=14, dtype=dtype)
+    ref = dy.float().T @ x.float()
+    dyd, xd = dy.to(DEV), x.to(DEV)
+    b = ops.ColBatch()
+    out = torch.empty(N, K, device=DEV)
+    ops.linear_wgrad(dyd, xd, out=out, split=split, reduce_on=b)
+    if dtype == torch.bfloat16:
+        assert len(b.jobs) == 1 and b.jobs[0][2] == L.lib().vit_linear_wgrad_nslabs(L.dt(dyd), M, N, K, split)
+    b.launch()
+    torch.cuda.synchronize()
+    _close(out, ref, 2e-5, "wgrad via batch")
+    imm = ops.linear_wgrad(dyd, xd, split=split)
+    _close(out, imm, 1e-6, "batch vs immediate reduction")
+
+
+@pytest.mark.parametrize("group", [1, 3, 8])
+def test_gemm_grouped_tile_walk(group):
+    """The banded tile walk (vit_gemm_group) is a bijection over the tiles: every output tile is
+    written exactly once for bands that divide the row tiles and for ragged last bands."""
+    lib = L.lib()
+    M, N, K = 197 * 13, 1536, 256       # 11 row tiles of 256 (the last ragged), 6 column tiles
+    x = _rnd(M, K, seed=45, dtype=torch.bfloat16)
+    w = _rnd(N, K, seed=46, scale=0.05, dtype=torch.bfloat16)
+    dy = _rnd(M, N, seed=47, dtype=torch.bfloat16)
+    lib.vit_gemm_group(group, group)
+    try:
+        _close(ops.linear_fwd(x.to(DEV), w.to(DEV), None, out_dtype=torch.float32), x.float() @ w.float().T, 1e-5,
+               "fwd grouped")
+        _close(ops.linear_dgrad(dy.to(DEV), w.to(DEV)), dy.float() @ w.float(), 1e-5, "dgrad grouped")
+    finally:
+        lib.vit_gemm_group(-1, -1)
+
+
 @pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
 def test_gemm_every_tile_config(variant):
     """Every kept MFMA configuration (forced through vit_gemm_variant) on ragged
@@ -290,6 +331,35 @@ def test_generic_gemm_odd_shapes(dtype):
     _close(ops.linear_dgrad(dy.to(DEV), w.to(DEV)), dy.float() @ w.float(), 1e-5, "generic dgrad")
     _close(ops.linear_wgrad(dy.to(DEV), x.to(DEV)), dy.float().T @ x.float(), 1e-5, "generic wgrad")
     _close(ops.linear_wgrad(dy.to(DEV), x.to(DEV), split=3), dy.float().T @ x.float(), 1e-5, "generic wgrad split")
+
+
+def test_colreduce_batch_matches_sums_and_is_deterministic():
+    """vit_colreduce_batch (one launch for a block's bias / LN-affine reductions): every job against
+    a float64 column sum, single-chunk and multi-chunk jobs (in-launch ticket combine), accumulate,
+    a non-vector job (N % 4 != 0: two-stage fallback), more than 16 jobs (two launches); two runs
+    bitwise equal; the ticket counters are left zero."""
+    cases = [(1, 768, 0), (50, 768, 1), (64, 2304, 0), (65, 3072, 0), (788, 3072, 1), (1576, 768, 0),
+             (256, 2304, 0), (130, 100, 0), (7, 30, 1)] + [(100 + 37 * i, 768, i % 2) for i in range(10)]
+    parts, outs, refs = [], [], []
+    for i, (S, N, acc) in enumerate(cases):
+        p = _rnd(S, N, seed=200 + i).to(DEV)
+        o = _rnd(N, seed=300 + i).to(DEV)
+        refs.append(p.double().sum(0) + (o.double() if acc else 0))
+        parts.append(p)
+        outs.append(o)
+    res = []
+    for rep in range(2):
+        b = ops.ColBatch()
+        os_ = [o.clone() for o in outs]
+        for p, o, (S, N, acc) in zip(parts, os_, cases):
+            b.add(p, S, N, o, accumulate=bool(acc))
+        b.launch()
+        torch.cuda.synchronize()
+        res.append(os_)
+    for i, (o1, o2, r) in enumerate(zip(res[0], res[1], refs)):
+        _close(o1, r.float(), 1e-5, f"job {i} {cases[i]}")
+        assert torch.equal(o1, o2), f"job {i} not reproducible"
+    assert int(ops._counters("colbatch", 1, DEV).abs().sum()) == 0
 
 
 def test_colsum():

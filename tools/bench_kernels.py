@@ -39,9 +39,12 @@ def main():
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--sweep", type=str, default="", help="comma list of GEMM variants to sweep (big::V<n>)")
     ap.add_argument("--torch", action="store_true", help="time torch.matmul (hipBLASLt) on the same shapes")
+    ap.add_argument("--groups", type=str, default="", help="comma list of tile-walk bands (vit_gemm_group) to time")
     a = ap.parse_args()
     if a.torch:
         return torch_ref(a)
+    if a.groups:
+        return groups(a, [int(v) for v in a.groups.split(",")])
     if a.sweep:
         return sweep(a, [int(v) for v in a.sweep.split(",")])
     dev = "cuda"
@@ -121,6 +124,49 @@ def torch_ref(a):
             t = timeit(fn, a.reps)
             print(json.dumps({"lib": "torch.matmul", "name": f"{kind}_{nm}", "ms": round(t * 1e3, 4),
                               "tflops": round(flop / t / 1e12, 1)}), flush=True)
+
+
+def groups(a, bands):
+    """Forward / input-gradient GEMMs (the step's epilogues) under each tile-walk band, interleaved
+    rounds in one process; results checked against the row-major walk."""
+    dev, bf = "cuda", torch.bfloat16
+    M, D, F = a.batch * 197, 768, 3072
+    r = lambda *s: torch.randn(*s, device=dev).to(bf)
+    cases = []
+    for nm, (K, Nout) in {"qkv": (D, 3 * D), "proj": (D, D), "fc1": (D, F), "fc2": (F, D)}.items():
+        x, w, dy = r(M, K), r(Nout, K) * 0.05, r(M, Nout)
+        b = torch.randn(Nout, device=dev)
+        flop = 2.0 * M * Nout * K
+        outb = torch.empty(M, Nout, device=dev, dtype=bf)
+        dxb = torch.empty(M, K, device=dev, dtype=bf)
+        if nm == "fc1":
+            act = torch.empty_like(outb)
+            cases.append(("fwd_fc1_gelu", flop, lambda x=x, w=w, o=outb, a_=act, b_=b:
+                          ops.linear_fwd(x, w, b_, epi=L.EPI_BIAS_GELU, out=o, act_out=a_), act))
+        else:
+            cases.append((f"fwd_{nm}", flop, lambda x=x, w=w, o=outb, b_=b: ops.linear_fwd(x, w, b_, out=o), outb))
+        if nm == "fc2":
+            pre = r(M, K)
+            cases.append(("dgrad_fc2_gelubwd", flop, lambda dy=dy, w=w, p_=pre, o=dxb:
+                          ops.linear_dgrad(dy, w, out_dtype=bf, epi=L.EPI_GELU_BWD, pre=p_, out=o), dxb))
+        else:
+            cases.append((f"dgrad_{nm}", flop, lambda dy=dy, w=w, o=dxb: ops.linear_dgrad(dy, w, out=o), dxb))
+    lib = L.lib()
+    lib.vit_gemm_group(0, 0)
+    ref = {}
+    for name, flop, fn, out in cases:
+        fn(); torch.cuda.synchronize(); ref[name] = out.float().clone()
+    table = {}
+    for rnd in range(2):
+        for g in bands:
+            lib.vit_gemm_group(g, g)
+            for name, flop, fn, out in cases:
+                t = timeit(fn, a.reps)
+                err = ((out.float() - ref[name]).abs().max() / ref[name].abs().max()).item()
+                table.setdefault(name, {}).setdefault(g, []).append(round(flop / t / 1e12, 1))
+                assert err == 0.0, (name, g, err)
+    lib.vit_gemm_group(-1, -1)
+    print("GROUPS", json.dumps({"batch": a.batch, "tflops": table}))
 
 
 def sweep(a, variants):

@@ -1613,12 +1613,17 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
   if (head_dim != 64 || N <= 0 || N > 288) return (int)hipErrorInvalidValue;
   const int D = H * 64;
   if (!delta_ws) return (int)hipErrorInvalidValue;
-  if (dbias && (partial == nullptr || partial_floats < vit_sdpa_bwd_partial_floats(B, N, D))) return (int)hipErrorInvalidValue;
-  if (dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_do % 8 == 0) && (ld_dqkv % 4 == 0) && (ld_o % 4 == 0)) {
+  // dbias == null with a partial buffer: leave the per-image [B][3D] partials for the caller (bf16 path)
+  const bool part_only = !dbias && partial;
+  if ((dbias || part_only) && (partial == nullptr || partial_floats < vit_sdpa_bwd_partial_floats(B, N, D)))
+    return (int)hipErrorInvalidValue;
+  const bool mfma_ok = dtype == VIT_BF16 && (ld_qkv % 8 == 0) && (ld_do % 8 == 0) && (ld_dqkv % 4 == 0) && (ld_o % 4 == 0);
+  if (part_only && !mfma_ok) return (int)hipErrorInvalidValue;
+  if (mfma_ok) {
     int nt = (N + 15) / 16;
     int rc = (int)hipErrorInvalidValue;
     switch (nt) {
-#define CASE(n) case n: rc = bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, causal, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, dbias ? partial : nullptr, s); break;
+#define CASE(n) case n: rc = bwd_mfma<n>(qkv, ld_qkv, D, B, H, N, scale, causal, o, ld_o, dout, ld_do, lse, delta_ws, dqkv, ld_dqkv, (dbias || part_only) ? partial : nullptr, s); break;
       NT_CASES(CASE)
 #undef CASE
     }

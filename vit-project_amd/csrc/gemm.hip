@@ -38,6 +38,7 @@ struct Epi {
   int n_patch;              // EPI_PATCH: patches per image (seq = n_patch + 1)
   int64_t slab;             // split-r: element offset of slab z
   float* csum;              // optional column sums of the epilogue output: [ceil(M/64)][N] partials (64-row groups)
+  int group_m;              // > 0: tiles walk column-major inside bands of group_m row tiles (L2 reuse of Q columns)
   int dbg;                  // timing experiments only (vit_gemm_variant(v + 100*bits)): 1 = no in-loop loads, 2 = no in-loop barriers, 4 = no epilogue, 16 = fragment epilogue
 };
 
@@ -577,6 +578,24 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Tile t of a tiles_i x tiles_j grid.  group_m == 0: row-major (consecutive t share a row tile,
+// so the P rows stay in the XCD's L2 while every Q column block streams past).  group_m > 0:
+// bands of group_m row tiles walked column-major, so the workgroups an XCD runs at once cover
+// group_m row tiles x a few column tiles and both operand blocks fit its 4 MiB L2.
+__device__ __forceinline__ void tile_coords(int t, int tiles_i, int tiles_j, int group_m, int& ti, int& tj) {
+  if (group_m <= 0) {
+    ti = t / tiles_j;
+    tj = t - ti * tiles_j;
+    return;
+  }
+  const int per = group_m * tiles_j;
+  const int g = t / per, r = t - g * per;
+  const int first = g * group_m;
+  const int gsz = min(tiles_i - first, group_m);
+  tj = r / gsz;
+  ti = first + (r - tj * gsz);
+}
+
 // One output tile (unit w of the 1-D (split, tile) space) of the fast bf16 GEMM.
 template <class C, int PL, int QL, int EPI, typename TO, typename TA>
 __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ldp, const bf16* __restrict__ Q,
@@ -585,10 +604,11 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
   constexpr int S = C::STAGES, BM = C::BM, BN = C::BN, BK = C::BK;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tiles_j = (N + BN - 1) / BN;
-  const int tiles = ((M + BM - 1) / BM) * tiles_j;
+  const int tiles_j = (N + BN - 1) / BN, tiles_i = (M + BM - 1) / BM;
+  const int tiles = tiles_i * tiles_j;
   const int z = w / tiles, t = w - z * tiles;
-  const int ti = t / tiles_j, tj = t - ti * tiles_j;
+  int ti, tj;
+  tile_coords(t, tiles_i, tiles_j, e.group_m, ti, tj);
   const int i0 = ti * BM, j0 = tj * BN;
   const int rb = z * r_chunk;
   const int re = min(R, rb + r_chunk);
@@ -1250,9 +1270,25 @@ static int launch_pers(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
   return 0;
 }
 
+// row-tile band of the tile walk per class (tile_coords); VIT_GEMM_GROUP_{FWD,DGRAD}=<row tiles> (A/B)
+// Default (-1): bands of 8 row tiles when the output is wide (N >= 2048) and the weight operand
+// does not fit beside the row blocks in an XCD's 4 MiB L2 (>= 4 MiB): the fc1 forward (GELU pair)
+// and the fc2 input gradient (GELU'), +3.5-4.5 % standalone at the half-batch shapes
+// (tools/bench_kernels.py --groups); the other shapes measured neutral or slightly slower.
+static int g_group[2] = {-2, -2};  // forward, dgrad; -2 = not yet read from the environment
+static int group_for(int pl, int ql, int N, int R) {
+  if (g_group[0] == -2) g_group[0] = env_variant("VIT_GEMM_GROUP_FWD");
+  if (g_group[1] == -2) g_group[1] = env_variant("VIT_GEMM_GROUP_DGRAD");
+  const int g = (pl == LAY_RC && ql == LAY_RC) ? g_group[0] : (pl == LAY_RC && ql == LAY_CR) ? g_group[1] : 0;
+  if (g >= 0) return g;
+  return (N >= 2048 && (int64_t)N * R * 2 >= ((int64_t)4 << 20)) ? 8 : 0;
+}
+
 template <int PL, int QL, int EPI, typename TO, typename TA>
 static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R,
-                       int split, const Epi& e, hipStream_t s) {
+                       int split, const Epi& e0, hipStream_t s) {
+  Epi e = e0;
+  if (split <= 1) e.group_m = group_for(PL, QL, N, R);
   constexpr bool pers_ok = PL == LAY_RC && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU ||
                                             EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
   const int v = pick_variant(PL, QL, M, N, R, split, pers_ok, EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD,
@@ -1414,6 +1450,10 @@ extern "C" {
 // launch, 0 when even 256 rows do not fit).
 int vit_gemm_rc_chunk_rows(int M, int64_t ld) { return rc_chunk_rows(M, ld); }
 
+// Tuning hook: row-tile band of the forward / dgrad tile walk (0 = row-major, -1 = per-shape default;
+// tile_coords).
+int vit_gemm_group(int fwd, int dgrad) { g_group[0] = fwd; g_group[1] = dgrad; return 0; }
+
 // Tuning hook: force GEMM configuration big::V<v> (-1 restores the per-shape heuristic).
 int vit_gemm_variant(int v) { g_variant = v; g_dbg = v >= 100 ? v / 100 : 0; return 0; }
 
@@ -1532,6 +1572,51 @@ int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t ldd
   t.C = dW; t.ldc = K;
   const size_t esz = dtype == VIT_BF16 ? 2 : 4;
   return gemm_any(EPI_ACC, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, M - R0, (const char*)dY + (size_t)R0 * lddy * esz,
+                  lddy, (const char*)X + (size_t)R0 * ldx * esz, ldx, 1, t, s, false);
+}
+
+// Number of fp32 slabs vit_linear_wgrad_partials writes for this shape and split.
+int vit_linear_wgrad_nslabs(int dtype, int M, int N, int K, int split) {
+  if (split < 1) split = 1;
+  if (M <= 0) return 0;
+  const int tail = M % 32;
+  const int R0 = M - tail;
+  if (R0 <= 0) return 1;
+  const int bk = dtype == VIT_BF16 ? 64 : f32m::BK;
+  const int r_chunk = r_chunk_for(R0, split, bk);
+  return (R0 + r_chunk - 1) / r_chunk;
+}
+
+// Weight gradient as split-K partials only: slabs[z][N][K] (f32, z < vit_linear_wgrad_nslabs) with
+// dW = sum_z slabs[z]; the caller reduces them (vit_colreduce_batch: S = nslabs, N = N*K), e.g. in
+// the one reduction launch of a block's backward.  The ragged M % 32 rows are added into the last slab.
+int vit_linear_wgrad_partials(int dtype, int M, int N, int K, const void* dY, int64_t lddy, const void* X,
+                              int64_t ldx, int split, float* slabs, int64_t slab_bytes, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  const int nz = vit_linear_wgrad_nslabs(dtype, M, N, K, split);
+  if (M <= 0 || nz <= 0) return (int)hipErrorInvalidValue;
+  if (slabs == nullptr || slab_bytes < (int64_t)nz * N * K * 4 || ((uintptr_t)slabs & 15)) return (int)hipErrorInvalidValue;
+  const int tail = M % 32;
+  const int R0 = M - tail;
+  Epi e = make_epi();
+  e.C = slabs; e.ldc = K; e.slab = (int64_t)N * K;
+  if (R0 > 0) {
+    const bool fast = any_fast_ok(dtype, LAY_CR, LAY_CR, N, K, R0, dY, X, lddy, ldx) &&
+                      (dtype == VIT_BF16 || f32_grid_ok(N, K, split));
+    // the MFMA and generic paths chunk the rows the same way (r_chunk_for with their BK; the generic
+    // TK = 64 = the bf16 BK) only on the bf16 path: elsewhere one slab per launch keeps nz exact
+    if (!fast && dtype != VIT_BF16) return (int)hipErrorInvalidValue;
+    const int rc = gemm_any(EPI_STORE, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, R0, dY, lddy, X, ldx, split, e, s, fast);
+    if (rc) return rc;
+  } else {
+    const int rc = (int)hipMemsetAsync(slabs, 0, (size_t)N * K * 4, s);
+    if (rc) return rc;
+  }
+  if (tail == 0) return 0;
+  Epi t = make_epi();
+  t.C = slabs + (int64_t)(nz - 1) * N * K; t.ldc = K;
+  const size_t esz = dtype == VIT_BF16 ? 2 : 4;
+  return gemm_any(EPI_ACC, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, tail, (const char*)dY + (size_t)R0 * lddy * esz,
                   lddy, (const char*)X + (size_t)R0 * ldx * esz, ldx, 1, t, s, false);
 }
 

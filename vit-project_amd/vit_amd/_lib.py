@@ -26,6 +26,7 @@ i32, i64, f32, vp = C.c_int, C.c_int64, C.c_float, C.c_void_p
 SIGNATURES = {
     "vit_abi_version": [],
     "vit_gemm_variant": [i32],
+    "vit_gemm_group": [i32, i32],
     "vit_gemm_rc_chunk_rows": [i32, i64],
     "vit_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, vp],
     "vit_linear_fwd": [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, i64, vp, vp, vp],
@@ -33,7 +34,11 @@ SIGNATURES = {
     "vit_linear_dgrad_partial_floats": [i32, i32],
     "vit_colreduce": [vp, i32, i32, vp, i32, vp, vp],
     "vit_colreduce_multi": [vp, i32, i32, i32, vp, vp, vp, i32, vp, vp],
+    "vit_colreduce_batch_sizes": [vp, i32, vp, vp],
+    "vit_colreduce_batch": [vp, i32, vp, i64, vp, i32, vp],
     "vit_linear_wgrad": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i32, vp, i64, vp],
+    "vit_linear_wgrad_nslabs": [i32, i32, i32, i32, i32],
+    "vit_linear_wgrad_partials": [i32, i32, i32, i32, vp, i64, vp, i64, i32, vp, i64, vp],
     "vit_colsum": [i32, i32, i32, vp, i64, vp, vp, i64, i32, vp],
     "vit_patch_embed_fwd": [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
     "vit_layer_norm_fwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, f32, vp],

@@ -89,6 +89,9 @@ _FUSED_RESID = [os.environ.get("VIT_FUSED_RESID", "1") != "0"]
 # ... and in fp32 compute with VIT_FUSED_RESID_F32=1 (bit-identical: the same f32 add, in the LayerNorm
 # instead of the epilogue; C3 fp32 measured 607 vs 609 img/s, so the f32 GEMM epilogue keeps it by default)
 _FUSED_RESID_F32 = [os.environ.get("VIT_FUSED_RESID_F32", "0") == "1"]
+# VIT_COL_BATCH=0: every bias / LayerNorm-affine reduction of a block's backward as its own launch(es)
+# (the round-2 schedule: ~9 launches per block) instead of one vit_colreduce_batch launch per block
+_COL_BATCH = [os.environ.get("VIT_COL_BATCH", "1") != "0"]
 
 
 def set_wgrad_overlap(enable: bool):
@@ -438,35 +441,42 @@ class _BlockFn(torch.autograd.Function):
         # MLP.  Bias gradients are column sums fused into the kernels that produce each
         # gradient: fc2.bias from the upstream LayerNorm backward (side channel), fc1.bias
         # from the GELU' dgrad epilogue, proj.bias from LN2 backward, qkv.bias from SDPA backward.
+        # every deferred column reduction of this block goes into ONE launch at its end (side stream)
+        rb = ops.ColBatch() if _COL_BATCH[0] else side
+        rbw = rb if _COL_BATCH[0] else None  # the weight gradients' split-K slab sums join the same launch
         if ng[12]:
             if dxo_sum is not None:  # the upstream LayerNorm backward's column sums (side stream)
-                side.run(lambda: ops.colreduce(dxo_sum, 1, D, g[12]))
+                if _COL_BATCH[0]:
+                    rb.add(dxo_sum.view(1, D), 1, D, g[12])
+                else:
+                    side.run(lambda: ops.colreduce(dxo_sum, 1, D, g[12]))
             else:
                 ops.colsum(dxo_c, out=g[12])
         if ng[11]:
-            side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g[11]))
+            side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g[11], reduce_on=rbw))
         dx = None
         if need_mlp_in:
-            dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=dact, dbias=g[10], reduce_on=side)
+            dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=dact, dbias=g[10], reduce_on=rb)
             if ng[9]:
-                side.run(lambda: ops.linear_wgrad(dpre, h2, out=g[9]))
+                side.run(lambda: ops.linear_wgrad(dpre, h2, out=g[9], reduce_on=rbw))
         if any(ng[0:9]):
             dh2 = ops.linear_dgrad(dpre, W1, out_dtype=T)
             dxm = torch.empty(M, D, dtype=torch.float32, device=dev)
             dxm_c = dxm if T == torch.float32 else torch.empty(M, D, dtype=T, device=dev)
             ops.layer_norm_bwd(xm, D, dh2, n2w.detach(), m2, r2, dxm, D, M, dres=dxo, ldres=D,
                                dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=g[7], dbeta=g[8],
-                               dsum=g[6], reduce_on=side)
+                               dsum=g[6], reduce_on=rb)
             # attention
             # block 0 (the patch rows' block, last in the backward): its last weight gradients are the tail
             tail = bool(compact_np)
             if ng[5]:
-                side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5], tail=tail))
+                side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5], tail=tail, reduce_on=rbw))
             if need_attn:
                 do = ops.linear_dgrad(dxm_c, Wproj, out_dtype=T)
-                dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g[4], causal=causal)
+                dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g[4], causal=causal,
+                                    reduce_on=rb if _COL_BATCH[0] else None)
                 if ng[3]:
-                    side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g[3], tail=tail))
+                    side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g[3], tail=tail, reduce_on=rbw))
             if need_h1:
                 dh1 = ops.linear_dgrad(dqkv, Wqkv, out_dtype=T)
                 dx = torch.empty(M, D, dtype=torch.float32, device=dev)
@@ -478,9 +488,12 @@ class _BlockFn(torch.autograd.Function):
                 dsum = None if (compact_np or not ng[0]) else torch.empty(D, dtype=torch.float32, device=dev)
                 ops.layer_norm_bwd(x2, D, dh1, n1w.detach(), m1, r1, dx, D, M, dres=dxm, ldres=D, dx_copy=dx_c,
                                    ld_copy=D, compact_np=compact_np, dgamma=g[1], dbeta=g[2], dsum=dsum,
-                                   reduce_on=side)
+                                   reduce_on=rb)
                 if ng[0] and (dx_c is not None or dsum is not None):
                     _put_copy(dx, dx_c, dsum)
+        if _COL_BATCH[0]:
+            side.run(rb.launch)
+            side.guard(*rb.parts)
         side.guard(dxo, dxo_c, dxo_sum, x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act,
                    *(v for v in (dpre, dxm, dxm_c, do, dqkv, dx) if v is not None))
         if cfg_defer_bwd(ctx):

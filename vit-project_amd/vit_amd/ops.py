@@ -98,6 +98,9 @@ def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, ou
          out.stride(0), ptr(pre), ptr(dbias), ptr(part), nfl, int(defer), _s(dy2d))
     if defer:
         rows = (M + 63) // 64
+        if isinstance(reduce_on, ColBatch):
+            reduce_on.add(part, rows, K, dbias)
+            return out
 
         def finish():
             _keep(part)
@@ -110,6 +113,58 @@ def colreduce(part, S, N, out, accumulate=False, scratch=None):
     """out[N] (+)= part[:S].sum(0) (partials from a fused epilogue)."""
     call("vit_colreduce", ptr(part), S, N, ptr(out), int(accumulate), ptr(scratch), _s(out))
     return out
+
+
+class ColBatch:
+    """Collects the deferred column reductions of one block's backward (bias and LayerNorm-affine
+    gradients from their producers' partial sums) and issues them as ONE vit_colreduce_batch launch
+    (``launch``, on whatever stream is current then -- the model's side stream).  The partial
+    buffers stay referenced until ``launch`` has been enqueued; the caller guards them for the
+    stream (``tensors``)."""
+
+    def __init__(self):
+        self.jobs = []
+        self.parts = []  # the partial buffers (guard them for the stream the launch runs on)
+        self.device = None
+
+    def add(self, part, S, N, out, accumulate=False):
+        """out[N] (+)= sum of the S rows of part ([S][N] f32, contiguous rows).  Only the output's
+        address is kept (gradient views must stay stealable by AccumulateGrad)."""
+        if out is None or S <= 0:
+            return
+        assert part.dtype == torch.float32 and out.dtype == torch.float32 and part.is_contiguous()
+        self.jobs.append((part.data_ptr(), out.data_ptr(), int(S), int(N), int(accumulate)))
+        self.parts.append(part)
+        self.device = part.device
+
+    def launch(self):
+        if not self.jobs:
+            return
+        import ctypes
+        import numpy as np
+        dev = self.device
+        arr = np.array(self.jobs, dtype=np.int64).reshape(-1)
+        jp = arr.ctypes.data_as(ctypes.c_void_p)
+        sf, nc = ctypes.c_int64(0), ctypes.c_int(0)
+        L.lib().vit_colreduce_batch_sizes(jp, len(self.jobs), ctypes.byref(sf), ctypes.byref(nc))
+        scratch = workspace("colbatch", max(16, sf.value * 4), dev)
+        cnt = _counters("colbatch", nc.value, dev)
+        call("vit_colreduce_batch", jp, len(self.jobs), ptr(scratch), sf.value, ptr(cnt), nc.value, L.stream_ptr(dev))
+        self.jobs = []
+
+
+_CNT = {}
+
+
+def _counters(name, n, device):
+    """Grow-only int32 ticket counters, zero-filled when allocated (the kernels that use them leave
+    them zero)."""
+    key = (name, torch.device(device))
+    t = _CNT.get(key)
+    if t is None or t.numel() < n:
+        t = torch.zeros(max(n, 64), dtype=torch.int32, device=device)
+        _CNT[key] = t
+    return t
 
 
 _WGRAD_WGS = [int(os.environ.get("VIT_WGRAD_WGS", "128"))]
@@ -130,8 +185,10 @@ def _wgrad_split(M, N, K, wgs=None):
     return max(1, min(want, M // 1024))
 
 
-def linear_wgrad(dy2d, x2d, out=None, split=None, tail=False):
-    """dW [N,K] (f32) = dy^T @ x,  dy [M,N], x [M,K].  tail: split for _WGRAD_TAIL_WGS workgroups."""
+def linear_wgrad(dy2d, x2d, out=None, split=None, tail=False, reduce_on=None):
+    """dW [N,K] (f32) = dy^T @ x,  dy [M,N], x [M,K].  tail: split for _WGRAD_TAIL_WGS workgroups.
+    ``reduce_on`` (a ColBatch): the split-K slabs go to a buffer of their own and their sum into
+    ``out`` becomes a job of that batch (no separate slab-reduce launch)."""
     M, N = dy2d.shape
     K = x2d.shape[1]
     assert x2d.shape[0] == M and x2d.dtype == dy2d.dtype
@@ -139,13 +196,21 @@ def linear_wgrad(dy2d, x2d, out=None, split=None, tail=False):
         out = torch.empty(N, K, dtype=torch.float32, device=dy2d.device)
     if split is None:
         split = _wgrad_split(M, N, K, _WGRAD_TAIL_WGS[0] if tail else None)
-    ws = workspace("wgrad", split * N * K * 4, dy2d.device) if split > 1 else None
+    defer = isinstance(reduce_on, ColBatch) and split > 1 and dy2d.dtype == torch.bfloat16
     probe = WGRAD_PROBE[0]
     if probe is not None:  # bench.py: HIP events around this launch, on the stream it runs on
         e0 = torch.cuda.Event(enable_timing=True)
         e0.record()
-    call("vit_linear_wgrad", L.dt(dy2d), M, N, K, ptr(dy2d), dy2d.stride(0), ptr(x2d), x2d.stride(0), ptr(out),
-         split, ptr(ws), 0 if ws is None else ws.numel(), _s(dy2d))
+    if defer:
+        nz = L.lib().vit_linear_wgrad_nslabs(L.dt(dy2d), M, N, K, split)
+        slabs = torch.empty(nz * N * K, dtype=torch.float32, device=dy2d.device)
+        call("vit_linear_wgrad_partials", L.dt(dy2d), M, N, K, ptr(dy2d), dy2d.stride(0), ptr(x2d), x2d.stride(0),
+             split, ptr(slabs), slabs.numel() * 4, _s(dy2d))
+        reduce_on.add(slabs.view(nz, N * K), nz, N * K, out)
+    else:
+        ws = workspace("wgrad", split * N * K * 4, dy2d.device) if split > 1 else None
+        call("vit_linear_wgrad", L.dt(dy2d), M, N, K, ptr(dy2d), dy2d.stride(0), ptr(x2d), x2d.stride(0), ptr(out),
+             split, ptr(ws), 0 if ws is None else ws.numel(), _s(dy2d))
     if probe is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
@@ -232,6 +297,11 @@ def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0
          nfl, int(defer), _s(x))
     if defer:
         nb = L.lib().vit_layer_norm_bwd_blocks(rows)
+        if isinstance(reduce_on, ColBatch):
+            for q, o in enumerate((dgamma, dbeta, dsum)):
+                if o is not None:
+                    reduce_on.add(part[q * nb * D:(q + 1) * nb * D], nb, D, o)
+            return
         sc = part[3 * nb * D:]
 
         def finish():
@@ -269,20 +339,25 @@ def sdpa_fwd(qkv2d, B, H, N, o=None, scale=None, lse=None, causal=False, fp8=Fal
     return o, lse
 
 
-def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None, causal=False, ws=""):
+def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None, causal=False, ws="", reduce_on=None):
     """dbias [3*H*64] (optional) receives the column sums of dqkv (the qkv bias gradient).
-    ``ws``: workspace-name suffix (calls running concurrently on different streams need their own)."""
+    ``ws``: workspace-name suffix (calls running concurrently on different streams need their own).
+    ``reduce_on`` (a ColBatch, bf16): the per-image bias partials are left for that batch to reduce."""
     if dqkv is None:
         dqkv = torch.empty_like(qkv2d)
     scale = 64 ** -0.5 if scale is None else scale
     delta = workspace("sdpa_delta" + ws, B * H * N * 4, qkv2d.device)
     part, nfl = None, 0
+    defer = dbias is not None and isinstance(reduce_on, ColBatch) and qkv2d.dtype == torch.bfloat16
     if dbias is not None:
         nfl = L.lib().vit_sdpa_bwd_partial_floats(B, N, H * 64)
-        part = workspace("sdpa_bias" + ws, nfl * 4, qkv2d.device)
+        part = (torch.empty(nfl, dtype=torch.float32, device=qkv2d.device) if defer
+                else workspace("sdpa_bias" + ws, nfl * 4, qkv2d.device))
     call("vit_sdpa_bwd", L.dt(qkv2d), B, H, N, 64, ptr(qkv2d), qkv2d.stride(0), ptr(o), o.stride(0), ptr(do),
-         do.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), ptr(delta), float(scale), int(causal), ptr(dbias),
-         ptr(part), nfl, _s(qkv2d))
+         do.stride(0), ptr(lse), ptr(dqkv), dqkv.stride(0), ptr(delta), float(scale), int(causal),
+         None if defer else ptr(dbias), ptr(part), nfl, _s(qkv2d))
+    if defer:
+        reduce_on.add(part, B, 3 * H * 64, dbias)
     return dqkv
 
 
