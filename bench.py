@@ -137,10 +137,25 @@ def cpu_baseline(seconds: float):
                       f"{el:.1f} s, torch CPU {threads} threads (the process's CPU share of {total})"}
 
 
+def _pmc_mfma_busy():
+    """MFMA-busy fraction of the weight-gradient class from the latest committed step counter
+    passes (profiles/r0N/pmc_step_classes*.json, tools/pmc_step_classes.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_step_classes*.json")))
+    for f in reversed(files):
+        try:
+            with open(f) as fh:
+                c = json.load(fh)["classes"]["gemm wgrad"]
+            return c.get("mfma_busy"), os.path.relpath(f, ROOT)
+        except (OSError, KeyError, ValueError):
+            continue
+    return None, None
+
+
 def _pmc_traffic(name):
     """HBM bytes per launch of a kernel from committed counter passes (tools/pmc_traffic.py;
     FETCH_SIZE doubled per the gfx950 correction), or None."""
-    for rnd in ("r02", "r01"):
+    for rnd in ("r03", "r02", "r01"):
         f = os.path.join(ROOT, "profiles", rnd, name)
         try:
             with open(f) as fh:
@@ -375,24 +390,33 @@ def main(a):
               "avg_launch_ms": round(tot_ms / per_step, 4), "flop_per_step": tot_fl,
               "tflops": round(tot_fl / (tot_ms * 1e-3) / 1e12, 1)}
 
-    # --- standalone leg of the same kernel: the fc1 weight gradient (dW1 = dpre^T h2, M = B*197,
-    #     N = 3072, K = 768) at the step's own split, alone on the GPU, HIP events on its stream
+    # --- standalone leg of the same kernel as the step runs it: the MLP weight-gradient pair
+    #     (dW2 = dy^T act, M = B*197, 768 x 3072, and dW1 = dpre^T h2, 3072 x 768) as one grouped
+    #     launch at the step's split, then its split-K slab sums (the block's reduction launch),
+    #     alone on the GPU, HIP events on its stream; both launches count in the time
     M = B * 197
-    dpre = torch.randn(M, 3072, device=dev).to(torch.bfloat16)
-    h2 = torch.randn(M, 768, device=dev).to(torch.bfloat16)
-    dw = torch.empty(3072, 768, device=dev)
+    bf = torch.bfloat16
+    dy2, act = torch.randn(M, 768, device=dev).to(bf), torch.randn(M, 3072, device=dev).to(bf)
+    dpre, h2 = torch.randn(M, 3072, device=dev).to(bf), torch.randn(M, 768, device=dev).to(bf)
+    dw2, dw1 = torch.empty(768, 3072, device=dev), torch.empty(3072, 768, device=dev)
+
+    def pair_step():
+        cb = ops.ColBatch()
+        ops.linear_wgrad_pair((dy2, act, dw2), (dpre, h2, dw1), cb)
+        cb.launch()
+
     with torch.cuda.stream(main_stream):
-        for _ in range(20):
-            ops.linear_wgrad(dpre, h2, out=dw)
+        for _ in range(10):
+            pair_step()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 20
         e0.record()
         for _ in range(reps):
-            ops.linear_wgrad(dpre, h2, out=dw)
+            pair_step()
         e1.record()
         torch.cuda.synchronize(dev)
     k_ms = e0.elapsed_time(e1) / reps
-    k_flop = 2.0 * M * 3072 * 768
+    k_flop = 2.0 * 2.0 * M * 3072 * 768
     k_tflops = k_flop / (k_ms * 1e-3) / 1e12
     red_ms = None
     if red_events:
@@ -408,21 +432,28 @@ def main(a):
     value = imgs / el
     ms = el / a.steps * 1e3
     step_tflops = value / world * STEP_FLOP_PER_IMG / 1e12
-    traffic, traffic_src = _pmc_traffic("pmc_traffic_wgrad_fc1.json")
+    traffic, traffic_src = _pmc_traffic("pmc_traffic_wgrad_pair.json")
+    mfma_busy, busy_src = _pmc_mfma_busy()
     if wg is not None:
-        roof = {"bound": "mfma", "kernel": "big::pp_kernel (split-K weight-gradient GEMM, 256x256x32 ping-pong) "
-                                           "+ its slab reduce: every bf16 dW = dY^T X of the step",
+        roof = {"bound": "mfma", "kernel": "big::pp_kernel2 / pp_kernel (split-K weight-gradient GEMM, 256x256x32 "
+                                           "ping-pong; fc2+fc1 and proj+qkv as grouped pairs): every bf16 dW = dY^T X "
+                                           "of the step",
                 "achieved": wg["tflops"], "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
                 "frac": round(wg["tflops"] / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                 "measured": "in-step: HIP events around each launch on the side stream it runs on, over the timed "
-                            "steps (its CUs are shared with the caller stream's kernels)",
+                            "steps (its CUs are shared with the caller stream's kernels); the split-K slab sums run "
+                            "in each block's single reduction launch, which the standalone leg includes",
                 "launches_per_step": wg["launches_per_step"], "ms_per_step": wg["ms_per_step"],
                 "avg_launch_ms": wg["avg_launch_ms"], "flop_per_step": wg["flop_per_step"],
-                "standalone": {"shape": "fc1 dW M=%d N=3072 K=768" % M, "ms": round(k_ms, 4),
+                "standalone": {"shape": "MLP pair dW2 (768x3072) + dW1 (3072x768), M=%d, grouped launch + slab-sum "
+                                        "launch" % M, "ms": round(k_ms, 4),
                                "achieved": round(k_tflops, 1), "frac": round(k_tflops / PEAK_BF16_TFLOPS, 4),
                                "flop_per_launch": k_flop},
-                "traffic_unit": "HBM bytes per standalone fc1 launch (FETCH_SIZE x2 + WRITE_SIZE, rocprofv3 --pmc "
-                                "passes, %s)" % traffic_src}
+                "traffic_unit": "HBM bytes per standalone pair (grouped launch + its slab sums; FETCH_SIZE x2 + "
+                                "WRITE_SIZE, rocprofv3 --pmc passes, %s)" % traffic_src,
+                "mfma_busy": mfma_busy,
+                "mfma_busy_unit": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8) of the weight-gradient "
+                                  "launches in the step's counter passes (dispatches serialized; %s)" % busy_src}
     else:
         roof = {"bound": "mfma", "kernel": "big::pp_kernel fc1 weight gradient, standalone",
                 "achieved": round(k_tflops, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",

@@ -48,8 +48,8 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
 int vit_gemm_variant(int v);
 
 /* Tuning hook: the forward / input-gradient GEMMs walk their tiles in bands of `fwd` / `dgrad`
- * row tiles, column-major inside a band (L2 reuse of the weight columns); 0 = row-major, -1 = the
- * per-shape default (bands of 8 for wide outputs with >= 4 MiB weights). */
+ * row tiles, column-major inside a band (L2 reuse of the weight columns); 0 = row-major (the
+ * default), -1 = the per-shape rule (bands of 8 for wide outputs with >= 4 MiB weights). */
 int vit_gemm_group(int fwd, int dgrad);
 
 /* Host-only query (no GPU call): rows per launch the bf16 MFMA path uses for a row-contiguous
@@ -85,6 +85,14 @@ int vit_linear_wgrad(int dtype, int M, int N, int K, const void* dY, int64_t ldd
 int vit_linear_wgrad_nslabs(int dtype, int M, int N, int K, int split);
 int vit_linear_wgrad_partials(int dtype, int M, int N, int K, const void* dY, int64_t lddy, const void* X,
                               int64_t ldx, int split, float* slabs, int64_t slab_bytes, void* stream);
+/* Two weight gradients of one block over the same M token rows (fc2 + fc1, or proj + qkv, from
+ * the autograd of VIT:142) as ONE launch of split-K partials: slabs_a / slabs_b as
+ * vit_linear_wgrad_partials for (Na, Ka) / (Nb, Kb) with the same split.  bf16, M % 32 == 0;
+ * otherwise hipErrorInvalidValue and nothing is launched. */
+int vit_linear_wgrad_partials2(int M, int split, int Na, int Ka, const void* dYa, int64_t lddya, const void* Xa,
+                               int64_t ldxa, float* slabs_a, int64_t bytes_a, int Nb, int Kb, const void* dYb,
+                               int64_t lddyb, const void* Xb, int64_t ldxb, float* slabs_b, int64_t bytes_b,
+                               void* stream);
 
 /* Column sums (bias gradients): out[N] = sum_i X[i][:] -- autograd of VIT:142. */
 int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, float* partial,

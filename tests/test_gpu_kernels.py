@@ -183,6 +183,25 @@ def test_linear_wgrad_partials_sum_to_dw(M, N, K, split, dtype):
     _close(out, imm, 1e-6, "batch vs immediate reduction")
 
 
+@pytest.mark.parametrize("M,tail", [(197 * 32, False), (197 * 32, True), (197 * 3, False)])
+def test_linear_wgrad_pair_matches_separate(M, tail):
+    """Two weight gradients as one grouped launch (fc2 + fc1 shapes at width 256 / 1024) against each
+    computed alone; a ragged M (197 * 3 = 591, M % 32 != 0) takes the one-by-one fallback."""
+    dya, xa = _rnd(M, 256, seed=60, dtype=torch.bfloat16), _rnd(M, 1024, seed=61, dtype=torch.bfloat16)
+    dyb, xb = _rnd(M, 1024, seed=62, dtype=torch.bfloat16), _rnd(M, 256, seed=63, dtype=torch.bfloat16)
+    ra, rb_ = dya.float().T @ xa.float(), dyb.float().T @ xb.float()
+    d = [t.to(DEV) for t in (dya, xa, dyb, xb)]
+    oa, ob = torch.empty(256, 1024, device=DEV), torch.empty(1024, 256, device=DEV)
+    b = ops.ColBatch()
+    ops.linear_wgrad_pair((d[0], d[1], oa), (d[2], d[3], ob), b, tail=tail)
+    if M % 32 == 0:
+        assert len(b.jobs) == 2  # grouped: the two slab sums are batch jobs
+    b.launch()
+    torch.cuda.synchronize()
+    _close(oa, ra, 2e-5, "pair a")
+    _close(ob, rb_, 2e-5, "pair b")
+
+
 @pytest.mark.parametrize("group", [1, 3, 8])
 def test_gemm_grouped_tile_walk(group):
     """The banded tile walk (vit_gemm_group) is a bijection over the tiles: every output tile is
@@ -198,7 +217,7 @@ def test_gemm_grouped_tile_walk(group):
                "fwd grouped")
         _close(ops.linear_dgrad(dy.to(DEV), w.to(DEV)), dy.float() @ w.float(), 1e-5, "dgrad grouped")
     finally:
-        lib.vit_gemm_group(-1, -1)
+        lib.vit_gemm_group(0, 0)
 
 
 @pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])

@@ -17,6 +17,13 @@ w = (torch.randn(F, D, device=dev) * 0.05).to(bf)
 for _ in range(reps):
     if which == "wgrad_fc1":
         ops.linear_wgrad(dy, x)
+    elif which == "wgrad_pair":  # the step's MLP weight-gradient pair + its slab sums (one batch launch)
+        if _ == 0:
+            dy2, act = torch.randn(M, D, device=dev).to(bf), torch.randn(M, F, device=dev).to(bf)
+            dw2, dw1 = torch.empty(D, F, device=dev), torch.empty(F, D, device=dev)
+        cb = ops.ColBatch()
+        ops.linear_wgrad_pair((dy2, act, dw2), (dy, x, dw1), cb)
+        cb.launch()
     elif which == "fwd_fc2":
         if _ == 0:
             a2 = torch.randn(M, F, device=dev).to(bf)

@@ -841,18 +841,17 @@ __device__ __forceinline__ void wait_vm_n(int n) {
   }
 }
 
+// unit w of the (split, tile) space of one ping-pong GEMM
 template <int S, int PL, int QL, int EPI, typename TO, typename TA>
-__global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, int64_t ldp,
-                                                    const bf16* __restrict__ Q, int64_t ldq,
-                                                    int M, int N, int R, int r_chunk, Epi e) {
+__device__ __forceinline__ void pp_tile(const bf16* __restrict__ P, int64_t ldp, const bf16* __restrict__ Q,
+                                        int64_t ldq, int M, int N, int R, int r_chunk, const Epi& e, int w,
+                                        char* smem) {
   using C = PP<S>;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wj = wave & 3;
   const int tiles_j = (N + 255) / 256;
   const int tiles = ((M + 255) / 256) * tiles_j;
-  const int w = xcd_remap(blockIdx.x, gridDim.x);
   const int z = w / tiles, t0 = w - z * tiles;
   const int ti = t0 / tiles_j, tj = t0 - ti * tiles_j;
   const int i0 = ti * 256, j0 = tj * 256;
@@ -989,6 +988,33 @@ __global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, 
     }
     if (e.csum && (a & 3) == 3) csum_flush<4>(e, cs, i0 + grp * 128 + (a - 3) * 16, M, N, j0 + wj * 64, lane);
   }
+}
+
+template <int S, int PL, int QL, int EPI, typename TO, typename TA>
+__global__ __launch_bounds__(512, 1) void pp_kernel(const bf16* __restrict__ P, int64_t ldp,
+                                                    const bf16* __restrict__ Q, int64_t ldq,
+                                                    int M, int N, int R, int r_chunk, Epi e) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  pp_tile<S, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, r_chunk, e, xcd_remap(blockIdx.x, gridDim.x), smem);
+}
+
+// Two weight gradients in one launch (grouped): units [0, nwg0) are problem 0's (split, tile)
+// space, the rest problem 1's.  Both reduce over the same token rows with the same split, so
+// every workgroup runs the same number of k-steps; the pair has twice the tiles of either, so
+// it fills the side stream's workgroup budget with half the split (half the fp32 slab traffic).
+struct PPProb {
+  const bf16* P; const bf16* Q; int64_t ldp, ldq;
+  int M, N, R, r_chunk, nwg;
+  Epi e;
+};
+template <int S, int PL, int QL, int EPI, typename TO, typename TA>
+__global__ __launch_bounds__(512, 1) void pp_kernel2(PPProb a, PPProb b) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  if (w < a.nwg)
+    pp_tile<S, PL, QL, EPI, TO, TA>(a.P, a.ldp, a.Q, a.ldq, a.M, a.N, a.R, a.r_chunk, a.e, w, smem);
+  else
+    pp_tile<S, PL, QL, EPI, TO, TA>(b.P, b.ldp, b.Q, b.ldq, b.M, b.N, b.R, b.r_chunk, b.e, w - a.nwg, smem);
 }
 
 // the configurations kept after the sweep (tools/bench_kernels.py --sweep; DESIGN.md
@@ -1271,14 +1297,15 @@ static int launch_pers(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
 }
 
 // row-tile band of the tile walk per class (tile_coords); VIT_GEMM_GROUP_{FWD,DGRAD}=<row tiles> (A/B)
-// Default (-1): bands of 8 row tiles when the output is wide (N >= 2048) and the weight operand
-// does not fit beside the row blocks in an XCD's 4 MiB L2 (>= 4 MiB): the fc1 forward (GELU pair)
-// and the fc2 input gradient (GELU'), +3.5-4.5 % standalone at the half-batch shapes
-// (tools/bench_kernels.py --groups); the other shapes measured neutral or slightly slower.
+// Bands of 8 row tiles help the wide-output GEMMs whose weight operand does not fit beside the
+// row blocks in an XCD's 4 MiB L2 (the fc1 forward GELU pair and the fc2 GELU' input gradient:
+// +3.5-4.5 % standalone at the half-batch shapes, tools/bench_kernels.py --groups) but measured
+// 0.5-1 % slower in the two-stream step (profiles/r03/ab_group_colbatch.txt), so the default is
+// the row-major walk; -1 selects that per-shape band rule.
 static int g_group[2] = {-2, -2};  // forward, dgrad; -2 = not yet read from the environment
 static int group_for(int pl, int ql, int N, int R) {
-  if (g_group[0] == -2) g_group[0] = env_variant("VIT_GEMM_GROUP_FWD");
-  if (g_group[1] == -2) g_group[1] = env_variant("VIT_GEMM_GROUP_DGRAD");
+  if (g_group[0] == -2) { const int v = env_variant("VIT_GEMM_GROUP_FWD"); g_group[0] = v == -1 ? 0 : v; }
+  if (g_group[1] == -2) { const int v = env_variant("VIT_GEMM_GROUP_DGRAD"); g_group[1] = v == -1 ? 0 : v; }
   const int g = (pl == LAY_RC && ql == LAY_RC) ? g_group[0] : (pl == LAY_RC && ql == LAY_CR) ? g_group[1] : 0;
   if (g >= 0) return g;
   return (N >= 2048 && (int64_t)N * R * 2 >= ((int64_t)4 << 20)) ? 8 : 0;
@@ -1618,6 +1645,48 @@ int vit_linear_wgrad_partials(int dtype, int M, int N, int K, const void* dY, in
   const size_t esz = dtype == VIT_BF16 ? 2 : 4;
   return gemm_any(EPI_ACC, dtype, VIT_F32, LAY_CR, LAY_CR, N, K, tail, (const char*)dY + (size_t)R0 * lddy * esz,
                   lddy, (const char*)X + (size_t)R0 * ldx * esz, ldx, 1, t, s, false);
+}
+
+// Two weight gradients over the same M token rows as ONE ping-pong launch (split-K partials only,
+// slabs as vit_linear_wgrad_partials for each): dW_a[Na,Ka] = dYa^T Xa, dW_b[Nb,Kb] = dYb^T Xb.
+// bf16, M % 32 == 0 and the MFMA operand rules for both; otherwise hipErrorInvalidValue (the caller
+// launches them one by one).
+int vit_linear_wgrad_partials2(int M, int split, int Na, int Ka, const void* dYa, int64_t lddya, const void* Xa,
+                               int64_t ldxa, float* slabs_a, int64_t bytes_a, int Nb, int Kb, const void* dYb,
+                               int64_t lddyb, const void* Xb, int64_t ldxb, float* slabs_b, int64_t bytes_b,
+                               void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (split < 1) split = 1;
+  if (M <= 0 || M % 32) return (int)hipErrorInvalidValue;
+  if (!fast_ok(VIT_BF16, LAY_CR, LAY_CR, Na, Ka, M, dYa, Xa, lddya, ldxa) ||
+      !fast_ok(VIT_BF16, LAY_CR, LAY_CR, Nb, Kb, M, dYb, Xb, lddyb, ldxb))
+    return (int)hipErrorInvalidValue;
+  const int nz = vit_linear_wgrad_nslabs(VIT_BF16, M, Na, Ka, split);
+  if (!slabs_a || !slabs_b || bytes_a < (int64_t)nz * Na * Ka * 4 || bytes_b < (int64_t)nz * Nb * Kb * 4 ||
+      ((uintptr_t)slabs_a & 15) || ((uintptr_t)slabs_b & 15))
+    return (int)hipErrorInvalidValue;
+  const int r_chunk = r_chunk_for(M, split, 64);
+  auto prob = [&](const void* dY, int64_t lddy, const void* X, int64_t ldx, int N, int K, float* slabs) {
+    big::PPProb p;
+    p.P = (const bf16*)dY; p.Q = (const bf16*)X; p.ldp = lddy; p.ldq = ldx;
+    p.M = N; p.N = K; p.R = M; p.r_chunk = r_chunk;
+    p.nwg = ((N + 255) / 256) * ((K + 255) / 256) * nz;
+    p.e = make_epi();
+    p.e.C = slabs; p.e.ldc = K; p.e.slab = (int64_t)N * K;
+    return p;
+  };
+  const big::PPProb a = prob(dYa, lddya, Xa, ldxa, Na, Ka, slabs_a), b = prob(dYb, lddyb, Xb, ldxb, Nb, Kb, slabs_b);
+  using C = big::PP<4>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL((big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>), dim3(a.nwg + b.nwg),
+                     dim3(C::THREADS), C::LDS, s, a, b);
+  VIT_CHECK_LAUNCH();
+  return 0;
 }
 
 // Column sum (bias grads): out[N] (f32) = sum_i X[i*ld + j]; partial buffer >= S*N floats

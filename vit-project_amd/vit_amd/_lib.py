@@ -39,6 +39,8 @@ SIGNATURES = {
     "vit_linear_wgrad": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i32, vp, i64, vp],
     "vit_linear_wgrad_nslabs": [i32, i32, i32, i32, i32],
     "vit_linear_wgrad_partials": [i32, i32, i32, i32, vp, i64, vp, i64, i32, vp, i64, vp],
+    "vit_linear_wgrad_partials2": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, i32, i32, vp, i64, vp, i64, vp,
+                                   i64, vp],
     "vit_colsum": [i32, i32, i32, vp, i64, vp, vp, i64, i32, vp],
     "vit_patch_embed_fwd": [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
     "vit_layer_norm_fwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, f32, vp],

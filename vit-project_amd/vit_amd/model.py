@@ -92,6 +92,9 @@ _FUSED_RESID_F32 = [os.environ.get("VIT_FUSED_RESID_F32", "0") == "1"]
 # VIT_COL_BATCH=0: every bias / LayerNorm-affine reduction of a block's backward as its own launch(es)
 # (the round-2 schedule: ~9 launches per block) instead of one vit_colreduce_batch launch per block
 _COL_BATCH = [os.environ.get("VIT_COL_BATCH", "1") != "0"]
+# VIT_WGRAD_PAIRS=0: each weight gradient as its own launch (with COL_BATCH) instead of fc2 + fc1 and
+# proj + qkv as one grouped launch each
+_WGRAD_PAIRS = [os.environ.get("VIT_WGRAD_PAIRS", "1") != "0"]
 
 
 def set_wgrad_overlap(enable: bool):
@@ -452,12 +455,17 @@ class _BlockFn(torch.autograd.Function):
                     side.run(lambda: ops.colreduce(dxo_sum, 1, D, g[12]))
             else:
                 ops.colsum(dxo_c, out=g[12])
-        if ng[11]:
+        # weight gradients in pairs over the same token rows (fc2 + fc1, proj + qkv): one grouped
+        # launch each, half the split-K slabs of two launches (VIT_WGRAD_PAIRS=0: one launch each)
+        pair_mlp = rbw is not None and _WGRAD_PAIRS[0] and ng[11] and ng[9] and need_mlp_in
+        if ng[11] and not pair_mlp:
             side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g[11], reduce_on=rbw))
         dx = None
         if need_mlp_in:
             dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=dact, dbias=g[10], reduce_on=rb)
-            if ng[9]:
+            if pair_mlp:
+                side.run(lambda: ops.linear_wgrad_pair((dxo_c, act, g[11]), (dpre, h2, g[9]), rbw))
+            elif ng[9]:
                 side.run(lambda: ops.linear_wgrad(dpre, h2, out=g[9], reduce_on=rbw))
         if any(ng[0:9]):
             dh2 = ops.linear_dgrad(dpre, W1, out_dtype=T)
@@ -469,13 +477,16 @@ class _BlockFn(torch.autograd.Function):
             # attention
             # block 0 (the patch rows' block, last in the backward): its last weight gradients are the tail
             tail = bool(compact_np)
-            if ng[5]:
+            pair_attn = rbw is not None and _WGRAD_PAIRS[0] and ng[5] and ng[3] and need_attn
+            if ng[5] and not pair_attn:
                 side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5], tail=tail, reduce_on=rbw))
             if need_attn:
                 do = ops.linear_dgrad(dxm_c, Wproj, out_dtype=T)
                 dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g[4], causal=causal,
                                     reduce_on=rb if _COL_BATCH[0] else None)
-                if ng[3]:
+                if pair_attn:
+                    side.run(lambda: ops.linear_wgrad_pair((dxm_c, o, g[5]), (dqkv, h1, g[3]), rbw, tail=tail))
+                elif ng[3]:
                     side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g[3], tail=tail, reduce_on=rbw))
             if need_h1:
                 dh1 = ops.linear_dgrad(dqkv, Wqkv, out_dtype=T)

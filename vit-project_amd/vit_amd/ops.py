@@ -218,6 +218,46 @@ def linear_wgrad(dy2d, x2d, out=None, split=None, tail=False, reduce_on=None):
     return out
 
 
+def linear_wgrad_pair(a, b, reduce_on, tail=False):
+    """Two weight gradients of a block over the same token rows, a = (dy, x, out), b likewise, as
+    ONE grouped launch of split-K partials whose slab sums become two jobs of ``reduce_on`` (a
+    ColBatch).  The split is chosen for the pair's tiles together (half the slabs of two separate
+    launches).  Falls back to two linear_wgrad calls when the pair does not meet the grouped
+    kernel's rules (bf16, M % 32 == 0, MFMA operand alignment)."""
+    (dya, xa, outa), (dyb, xb, outb) = a, b
+    M, Na = dya.shape
+    Ka, Nb, Kb = xa.shape[1], dyb.shape[1], xb.shape[1]
+    ok = (isinstance(reduce_on, ColBatch) and dya.dtype == torch.bfloat16 and dyb.dtype == torch.bfloat16
+          and xa.dtype == dya.dtype and xb.dtype == dyb.dtype and dyb.shape[0] == M and M % 32 == 0)
+    if ok:
+        tiles = ((Na + 255) // 256) * ((Ka + 255) // 256) + ((Nb + 255) // 256) * ((Kb + 255) // 256)
+        wgs = _WGRAD_TAIL_WGS[0] if tail else _WGRAD_WGS[0]
+        split = max(1, min(max(1, round(wgs / tiles)), M // 1024))
+        nz = L.lib().vit_linear_wgrad_nslabs(L.BF16, M, Na, Ka, split)
+        sa = torch.empty(nz * Na * Ka, dtype=torch.float32, device=dya.device)
+        sb = torch.empty(nz * Nb * Kb, dtype=torch.float32, device=dya.device)
+        probe = WGRAD_PROBE[0]
+        if probe is not None:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+        rc = L.lib().vit_linear_wgrad_partials2(M, split, Na, Ka, ptr(dya), dya.stride(0), ptr(xa), xa.stride(0),
+                                                ptr(sa), sa.numel() * 4, Nb, Kb, ptr(dyb), dyb.stride(0), ptr(xb),
+                                                xb.stride(0), ptr(sb), sb.numel() * 4, _s(dya))
+        if rc not in (0, 1):  # 1 = hipErrorInvalidValue: the pair does not fit the grouped kernel
+            L.check(rc, "vit_linear_wgrad_partials2")
+        if rc == 0:
+            if probe is not None:
+                e1 = torch.cuda.Event(enable_timing=True)
+                e1.record()
+                probe.append((e0, e1, 2.0 * M * (Na * Ka + Nb * Kb), True))
+            reduce_on.add(sa.view(nz, Na * Ka), nz, Na * Ka, outa)
+            reduce_on.add(sb.view(nz, Nb * Kb), nz, Nb * Kb, outb)
+            return outa, outb
+    linear_wgrad(dya, xa, out=outa, tail=tail, reduce_on=reduce_on)
+    linear_wgrad(dyb, xb, out=outb, tail=tail, reduce_on=reduce_on)
+    return outa, outb
+
+
 # bench.py's live roofline of the weight-gradient GEMMs: a list to collect
 # (start event, end event, flop, on the MFMA path) per vit_linear_wgrad launch, or None
 WGRAD_PROBE = [None]
