@@ -5,10 +5,10 @@
 // A job is out[N] (+)= sum_r part[r][N] over the S partial rows a producing kernel wrote (the
 // GEMM epilogues' 64-row column sums, the LayerNorm backward's per-block partials, the attention
 // backward's per-image sums, the weight gradients' split-K slabs).
-//   * short jobs (S <= 16: the split-K slabs, S = 4..14 over N*K ~ 2.4 M columns): a workgroup
+//   * short jobs (S <= 8: the split-K slabs of the weight-gradient pairs, 2..7 over ~2.4 M columns): a workgroup
 //     takes 2048 columns, each lane 2 x 4 of them, and adds the S rows in row order (the order of
 //     the former separate slab-reduce kernel, so the weight gradients are bit-identical to it);
-//   * tall jobs (S > 16): workgroup = 64 partial rows x 256 columns (4 waves x 16 rows, one f32x4
+//   * tall jobs (S > 8): workgroup = 64 partial rows x 256 columns (4 waves x 16 rows, one f32x4
 //     per lane per row, all 16 loads in flight at once); a job with more than 64 rows has several
 //     such chunks per 256-column strip: each chunk publishes its partial strip (agent-scope
 //     release, then a ticket on the strip's counter) and the workgroup that draws the last ticket
@@ -22,7 +22,7 @@
 
 namespace {
 constexpr int CB_MAXJ = 16, CB_ROWS = 64, CB_COLS = 256;
-constexpr int CB_SHORT = 16, CB_SHORT_COLS = 2048;  // short jobs: rows, columns per workgroup
+constexpr int CB_SHORT = 8, CB_SHORT_COLS = 2048;  // short jobs: rows, columns per workgroup
 struct CbJob {
   const float* part;
   float* out;
@@ -54,14 +54,24 @@ __global__ __launch_bounds__(256) void colreduce_batch_kernel(CbJobs jobs, float
   while (k + 1 < jobs.n && bid >= jobs.j[k + 1].wg0) ++k;
   const CbJob& J = jobs.j[k];
   const int local = bid - J.wg0;
-  if (J.S <= CB_SHORT) {  // rows added in row order, 2 x 4 columns per lane
+  if (J.S <= CB_SHORT) {  // rows added in row order, 2 x 4 columns per lane, all loads in flight
+    f32x4 a[2], v[2][CB_SHORT];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = local * CB_SHORT_COLS + (u * 256 + threadIdx.x) * 4;
+#pragma unroll
+      for (int r = 0; r < CB_SHORT; ++r)
+        if (r < J.S && c < J.N) v[u][r] = *reinterpret_cast<const f32x4*>(J.part + (int64_t)r * J.N + c);
+    }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int c = local * CB_SHORT_COLS + (u * 256 + threadIdx.x) * 4;
       if (c < J.N) {
-        f32x4 a = *reinterpret_cast<const f32x4*>(J.part + c);
-        for (int r = 1; r < J.S; ++r) a += *reinterpret_cast<const f32x4*>(J.part + (int64_t)r * J.N + c);
-        store_out(J.out, c, J.N, a, J.accumulate);
+        a[u] = v[u][0];
+#pragma unroll
+        for (int r = 1; r < CB_SHORT; ++r)
+          if (r < J.S) a[u] += v[u][r];
+        store_out(J.out, c, J.N, a[u], J.accumulate);
       }
     }
     return;
@@ -110,9 +120,19 @@ __global__ __launch_bounds__(256) void colreduce_batch_kernel(CbJobs jobs, float
   __syncthreads();
   // the chunk partials in chunk order, 4 columns per lane of wave 0 (the other waves idle)
   if (w == 0 && cok) {
+    // eight loads in flight per step (a dependent load per chunk would pay the L2 latency 25 times);
+    // the adds stay in chunk order
     const float* base = scratch + J.scr0 + c;
     f32x4 a = *reinterpret_cast<const f32x4*>(base);
-    for (int q = 1; q < J.chunks; ++q) a += *reinterpret_cast<const f32x4*>(base + (int64_t)q * J.N);
+    int q = 1;
+    for (; q + 8 <= J.chunks; q += 8) {
+      f32x4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = *reinterpret_cast<const f32x4*>(base + (int64_t)(q + u) * J.N);
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a += v[u];
+    }
+    for (; q < J.chunks; ++q) a += *reinterpret_cast<const f32x4*>(base + (int64_t)q * J.N);
     store_out(J.out, c, J.N, a, J.accumulate);
   }
 }

@@ -850,10 +850,20 @@ __device__ __forceinline__ void pp_tile(const bf16* __restrict__ P, int64_t ldp,
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wj = wave & 3;
-  const int tiles_j = (N + 255) / 256;
-  const int tiles = ((M + 255) / 256) * tiles_j;
+  const int tiles_j = (N + 255) / 256, tiles_i = (M + 255) / 256;
+  const int tiles = tiles_i * tiles_j;
   const int z = w / tiles, t0 = w - z * tiles;
-  const int ti = t0 / tiles_j, tj = t0 - ti * tiles_j;
+  // walk along the longer tile dimension, so an XCD's run of consecutive units (one split) covers
+  // all the short-side blocks and a band of the long side: for the 768 x 3072 fc2 weight gradient
+  // (3 x 12 tiles) 18 units = 3 x 6 tiles read 9 operand blocks instead of 2 x 12 = 14
+  int ti, tj;
+  if (tiles_j > tiles_i) {
+    tj = t0 / tiles_i;
+    ti = t0 - tj * tiles_i;
+  } else {
+    ti = t0 / tiles_j;
+    tj = t0 - ti * tiles_j;
+  }
   const int i0 = ti * 256, j0 = tj * 256;
   const int rb = z * r_chunk;
   const int re = min(R, rb + r_chunk);
