@@ -52,6 +52,14 @@ int vit_gemm_variant(int v);
  * default), -1 = the per-shape rule (bands of 8 for wide outputs with >= 4 MiB weights). */
 int vit_gemm_group(int fwd, int dgrad);
 
+/* Stream-K workspace for the fp32 MFMA GEMMs launched on `stream` (the reference-precision C3 path,
+ * NEWP:274): part >= 4 * CUs * 128*128 floats, counters >= 2 * CUs ints, zero-filled before first use
+ * (kernels leave them zero).  With it, an f32 GEMM whose tile count would leave a ragged last round
+ * (C3's 128.5 row tiles) runs as 2 * CUs persistent workgroups sharing the k-steps equally; cut
+ * tiles combine in-launch in a fixed order.  part == NULL removes the stream's entry (host-only); past
+ * 32 registered streams a new stream keeps the plain launch. */
+int vit_gemm_streamk_workspace(void* stream, float* part, int64_t part_bytes, int* counters, int ncounters);
+
 /* Host-only query (no GPU call): rows per launch the bf16 MFMA path uses for a row-contiguous
  * operand of M rows x ld elements (its staging offsets are 32-bit: larger operands are split
  * into row chunks, a multiple of 256 rows each); M when one launch fits, 0 if none does. */

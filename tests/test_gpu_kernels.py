@@ -286,6 +286,49 @@ def test_f32_mfma_gemm_every_layout_and_epilogue(M, N, K):
            1e-5, "wgrad ragged")
 
 
+@pytest.mark.parametrize("M,N,K", [(64 * 257, 1024, 256), (64 * 257, 3072, 128), (600 * 16, 1024, 96)])
+def test_f32_gemm_streamk_matches_reference(M, N, K):
+    """fp32 MFMA GEMM in its stream-K form (C3's ragged 128.5-row-tile shapes: 2*CUs persistent
+    workgroups, cut tiles combined in-launch): forward with bias, QuickGELU pair, residual, and the
+    input gradient with fused bias sums, against float64 references; the same launch without the
+    stream's workspace (one tile per workgroup) agrees to rounding; two stream-K runs are bitwise
+    equal."""
+    from vit_amd import ops as O
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(M, K, device=DEV, generator=g)
+    w = torch.randn(N, K, device=DEV, generator=g) * 0.05
+    b = torch.randn(N, device=DEV, generator=g)
+    ref = (x.double() @ w.double().T + b.double())
+    y1 = O.linear_fwd(x, w, b, out_dtype=torch.float32)
+    y2 = O.linear_fwd(x, w, b, out_dtype=torch.float32)
+    assert torch.equal(y1, y2)
+    _close(y1, ref.float(), 1e-5, "sk fwd")
+    dq, aq = O.linear_fwd(x, w, b, epi=L.EPI_BIAS_QGELU)
+    s = torch.sigmoid(1.702 * ref)
+    _close(aq, (ref * s).float(), 1e-5, "sk qgelu")
+    r = torch.randn(M, N, device=DEV, generator=g)
+    o = O.linear_fwd(x, w, b, epi=L.EPI_RESID, resid=r)
+    _close(o, (ref + r.double()).float(), 1e-5, "sk resid")
+    dy = torch.randn(M, N, device=DEV, generator=g)
+    db = torch.empty(K, device=DEV)
+    dx = O.linear_dgrad(dy, w, out_dtype=torch.float32, dbias=db)
+    dref = dy.double() @ w.double()
+    _close(dx, dref.float(), 1e-5, "sk dgrad")
+    _close(db, dref.sum(0).float(), 1e-5, "sk dgrad bias sums")
+    # without the stream's workspace: the plain launch
+    st = L.stream_ptr(torch.device(DEV))
+    L.lib().vit_gemm_streamk_workspace(st, None, 0, None, 0)
+    O._SK.pop(st, None)
+    try:
+        plain = torch.empty_like(y1)
+        L.call("vit_linear_fwd", L.F32, L.F32, L.EPI_STORE, M, N, K, x.data_ptr(), K, w.data_ptr(), b.data_ptr(),
+               plain.data_ptr(), N, None, None, st)
+        torch.cuda.synchronize()
+        _close(plain, y1, 1e-6, "plain vs stream-K")
+    finally:
+        O._streamk(torch.device(DEV))
+
+
 @pytest.mark.parametrize("K", [448, 768])
 def test_gemm_persistent_many_tiles(K):
     """The persistent forward / dgrad kernel (variant 10) with more tiles than CUs, so the

@@ -1349,6 +1349,23 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
   }
 }
 
+// Stream-K workspaces registered per stream by the host (vit_gemm_streamk_workspace): the cut-tile
+// fragment images (2 x 64 KiB per workgroup) and one ticket counter per workgroup boundary.
+struct SkWs { hipStream_t s; float* part; int64_t part_bytes; int* cnt; int ncnt; };
+static SkWs g_sk[32];
+static int g_nsk = 0;
+static int g_sk_mode = -2;  // VIT_GEMM_STREAMK: 0 off, 1 on (default: on where it removes a ragged round)
+static const SkWs* sk_for(hipStream_t s) {
+  for (int i = 0; i < g_nsk; ++i)
+    if (g_sk[i].s == s) return &g_sk[i];
+  return nullptr;
+}
+// fraction of the last round's workgroup slots a plain launch of `tiles` leaves empty
+static double ragged_waste(int64_t tiles, int slots) {
+  const int64_t rounds = (tiles + slots - 1) / slots;
+  return 1.0 - (double)tiles / (double)(rounds * slots);
+}
+
 template <int PL, int QL, int EPI, typename TO>
 static int launch_f32(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
                       const Epi& e, hipStream_t s) {
@@ -1356,7 +1373,24 @@ static int launch_f32(const void* P, int64_t ldp, const void* Q, int64_t ldq, in
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)f32m::gemm_kernel<PL, QL, EPI, TO, float>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, f32m::LDS);
+    (void)hipFuncSetAttribute((const void*)f32m::gemm_sk_kernel<PL, QL, EPI, TO, float>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, f32m::LDS + 16);
     attr = true;
+  }
+  if (g_sk_mode == -2) {
+    const char* v = getenv("VIT_GEMM_STREAMK");
+    g_sk_mode = v ? atoi(v) : 1;
+  }
+  const int64_t tiles = (int64_t)((M + f32m::BM - 1) / f32m::BM) * ((N + f32m::BN - 1) / f32m::BN);
+  const int G = 2 * num_cus();  // two workgroups per CU
+  if (split <= 1 && g_sk_mode == 1 && R % f32m::BK == 0 && tiles >= G && ragged_waste(tiles, G) > 0.03) {
+    const SkWs* w = sk_for(s);
+    if (w && w->ncnt >= G && w->part_bytes >= (int64_t)G * 2 * f32m::BM * f32m::BN * 4) {
+      hipLaunchKernelGGL((f32m::gemm_sk_kernel<PL, QL, EPI, TO, float>), dim3(G), dim3(f32m::THREADS),
+                         f32m::LDS + 16, s, (const float*)P, ldp, (const float*)Q, ldq, M, N, R, e, w->part, w->cnt);
+      VIT_CHECK_LAUNCH();
+      return 0;
+    }
   }
   const int r_chunk = r_chunk_for(R, split, f32m::BK);
   const int nz = (R + r_chunk - 1) / r_chunk;
@@ -1486,6 +1520,26 @@ extern "C" {
 // rows per launch for an RC operand of M rows and `ld` elements per row (M when it fits one
 // launch, 0 when even 256 rows do not fit).
 int vit_gemm_rc_chunk_rows(int M, int64_t ld) { return rc_chunk_rows(M, ld); }
+
+// Stream-K workspace for the f32 MFMA GEMMs launched on `stream` (C3's 128.5-row-tile shapes):
+// part >= 2 * CUs * 2 * 128*128 floats, counters >= 2 * CUs ints zero-filled before first use (the
+// kernel leaves them zero).  part == NULL removes the stream's entry.  Without an entry the plain
+// one-tile-per-workgroup launch runs.
+int vit_gemm_streamk_workspace(void* stream, float* part, int64_t part_bytes, int* counters, int ncounters) {
+  hipStream_t s = (hipStream_t)stream;
+  for (int i = 0; i < g_nsk; ++i)
+    if (g_sk[i].s == s) {
+      if (part == nullptr) {
+        g_sk[i] = g_sk[--g_nsk];
+        return 0;
+      }
+      g_sk[i] = SkWs{s, part, part_bytes, counters, ncounters};
+      return 0;
+    }
+  if (part == nullptr || g_nsk == 32) return 0;  // a full registry: the stream keeps the plain launch
+  g_sk[g_nsk++] = SkWs{s, part, part_bytes, counters, ncounters};
+  return 0;
+}
 
 // Tuning hook: row-tile band of the forward / dgrad tile walk (0 = row-major, -1 = per-shape default;
 // tile_coords).

@@ -48,6 +48,21 @@ def _keep(t: torch.Tensor):
 # GEMMs
 # ----------------------------------------------------------------------------
 
+_SK = {}  # stream handle -> (part, counters) registered with vit_gemm_streamk_workspace
+
+
+def _streamk(device):
+    """Register (once per stream) the stream-K workspace the f32 MFMA GEMMs use on the current stream."""
+    st = L.stream_ptr(device)
+    if st in _SK:
+        return
+    g = 2 * torch.cuda.get_device_properties(device).multi_processor_count
+    part = torch.empty(g * 2 * 128 * 128, dtype=torch.float32, device=device)
+    cnt = torch.zeros(g, dtype=torch.int32, device=device)
+    call("vit_gemm_streamk_workspace", st, ptr(part), part.numel() * 4, ptr(cnt), g)
+    _SK[st] = (part, cnt)
+
+
 def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, resid=None, act_out=None):
     """y = epi(x @ w^T + bias).  x2d [M,K] (row stride x2d.stride(0)), w [N,K] contiguous.
     EPI_BIAS_GELU / EPI_BIAS_QGELU return (act'(pre), act(pre)) with pre = x @ w^T + bias."""
@@ -68,6 +83,8 @@ def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, res
     if epi == L.EPI_RESID:
         assert resid is not None and resid.dtype == torch.float32 and out.dtype == torch.float32
         assert resid.stride(0) == out.stride(0)
+    if x2d.dtype == torch.float32:
+        _streamk(x2d.device)
     call("vit_linear_fwd", L.dt(x2d), L.dt(out), epi, M, N, K, ptr(x2d), x2d.stride(0), ptr(w), ptr(bias),
          ptr(out), out.stride(0), ptr(resid), ptr(act_out), _s(x2d))
     return (out, act_out) if epi in (L.EPI_BIAS_GELU, L.EPI_BIAS_QGELU) else out
@@ -94,6 +111,8 @@ def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, ou
         # a deferred reduction reads the partials later on another stream: own buffer
         part = (torch.empty(nfl, dtype=torch.float32, device=dy2d.device) if defer
                 else workspace("dgrad_bias", nfl * 4, dy2d.device))
+    if dy2d.dtype == torch.float32:
+        _streamk(dy2d.device)
     call("vit_linear_dgrad", L.dt(dy2d), L.dt(out), epi, M, N, K, ptr(dy2d), dy2d.stride(0), ptr(w), ptr(out),
          out.stride(0), ptr(pre), ptr(dbias), ptr(part), nfl, int(defer), _s(dy2d))
     if defer:
@@ -519,6 +538,8 @@ def gemm(P, p_layout, Q, q_layout, M, N, R, out=None, out_dtype=torch.float32, b
     assert P.dtype == Q.dtype and P.stride(-1) == 1 and Q.stride(-1) == 1
     if out is None:
         out = torch.empty(M, N, dtype=out_dtype, device=P.device)
+    if P.dtype == torch.float32:
+        _streamk(P.device)
     call("vit_gemm", L.dt(P), L.dt(out), p_layout, q_layout, L.EPI_STORE, M, N, R, ptr(P), P.stride(0), ptr(Q),
          Q.stride(0), ptr(out), out.stride(0), ptr(bias), None, 0, None, 1, _s(P))
     return out
