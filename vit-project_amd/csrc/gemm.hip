@@ -1354,7 +1354,7 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
 struct SkWs { hipStream_t s; float* part; int64_t part_bytes; int* cnt; int ncnt; };
 static SkWs g_sk[32];
 static int g_nsk = 0;
-static int g_sk_mode = -2;  // VIT_GEMM_STREAMK: 0 off, 1 on (default: on where it removes a ragged round)
+static int g_sk_mode = -2;  // VIT_GEMM_STREAMK: 0 off, 1 on (default: on where it removes a ragged round), 2 all k-steps shared
 static const SkWs* sk_for(hipStream_t s) {
   for (int i = 0; i < g_nsk; ++i)
     if (g_sk[i].s == s) return &g_sk[i];
@@ -1383,11 +1383,15 @@ static int launch_f32(const void* P, int64_t ldp, const void* Q, int64_t ldq, in
   }
   const int64_t tiles = (int64_t)((M + f32m::BM - 1) / f32m::BM) * ((N + f32m::BN - 1) / f32m::BN);
   const int G = 2 * num_cus();  // two workgroups per CU
-  if (split <= 1 && g_sk_mode == 1 && R % f32m::BK == 0 && tiles >= G && ragged_waste(tiles, G) > 0.03) {
+  if (split <= 1 && g_sk_mode >= 1 && R % f32m::BK == 0 && tiles >= G && ragged_waste(tiles, G) > 0.03) {
     const SkWs* w = sk_for(s);
     if (w && w->ncnt >= G && w->part_bytes >= (int64_t)G * 2 * f32m::BM * f32m::BN * 4) {
+      // tile-aligned rounds, then the last full round plus the remainder shared by k-steps
+      // (VIT_GEMM_STREAMK=2: every tile shared by k-steps)
+      const int dp_rounds = g_sk_mode == 2 ? 0 : (int)(tiles / G) - 1;
       hipLaunchKernelGGL((f32m::gemm_sk_kernel<PL, QL, EPI, TO, float>), dim3(G), dim3(f32m::THREADS),
-                         f32m::LDS + 16, s, (const float*)P, ldp, (const float*)Q, ldq, M, N, R, e, w->part, w->cnt);
+                         f32m::LDS + 16, s, (const float*)P, ldp, (const float*)Q, ldq, M, N, R, dp_rounds, e,
+                         w->part, w->cnt);
       VIT_CHECK_LAUNCH();
       return 0;
     }
