@@ -136,6 +136,10 @@ int vit_cls_pos_fill(int B, int S, int D, float* x, const float* cls, const floa
 /* d pos_embed [S,D] = sum_b dx[b]; d cls_token = d pos_embed[0]. */
 int vit_pos_grad(int B, int S, int D, const float* dx, float* dpos, float* dcls, void* stream);
 
+/* Tuning hook: LayerNorm backward form for D % 256 == 0 -- 1 = software-pipelined (next row's loads
+ * issued before this row's stores; default), 0 = the plain row loop.  Equal to rounding. */
+int vit_layer_norm_bwd_variant(int v);
+
 /* F.layer_norm forward (timm norm1/norm2/norm, eps 1e-6), one wave per row; saves mean/rstd. */
 int vit_layer_norm_fwd(int dtype_x, int dtype_y, int rows, int D, const void* x, int64_t ldx, void* y,
                        int64_t ldy, const float* w, const float* b, float* mean, float* rstd, float eps,

@@ -514,6 +514,38 @@ def test_add_layer_norm_fwd(D):
     _close(yf, torch.nn.functional.layer_norm(sf, (D,), w, b, 1e-6), 1e-5, "f32 ln")
 
 
+@pytest.mark.parametrize("dyt", [torch.bfloat16, torch.float32])
+def test_layer_norm_bwd_pipelined_matches_plain(dyt):
+    """The software-pipelined backward (two row buffers per wave) against the plain row loop:
+    dx, bf16 copy and dgamma / dbeta / dsum to rounding at the step's row count per workgroup,
+    with ragged workgroups (rows not a multiple of 4 or of the rows per workgroup)."""
+    M, D = 4097, 768
+    x = _rnd(M, D, seed=40, scale=2.0).to(DEV)
+    w = (1 + _rnd(D, seed=41, scale=0.2)).to(DEV)
+    b = _rnd(D, seed=42, scale=0.1).to(DEV)
+    dy = _rnd(M, D, seed=43).to(DEV).to(dyt)
+    dres = _rnd(M, D, seed=44).to(DEV)
+    _, mean, rstd = ops.layer_norm_fwd(x, w, b, 1e-6, torch.float32)
+    outs = []
+    try:
+        for v in (0, 1):
+            L.lib().vit_layer_norm_bwd_variant(v)
+            dx = torch.empty(M, D, device=DEV)
+            cp = torch.empty(M, D, dtype=torch.bfloat16, device=DEV)
+            dg, db, ds = (torch.empty(D, device=DEV) for _ in range(3))
+            ops.layer_norm_bwd(x, D, dy, w, mean, rstd, dx, D, M, dres=dres, ldres=D, dx_copy=cp, ld_copy=D,
+                               dgamma=dg, dbeta=db, dsum=ds)
+            torch.cuda.synchronize()
+            outs.append((dx, cp, dg, db, ds))
+    finally:
+        L.lib().vit_layer_norm_bwd_variant(1)
+    for a, c, nm in zip(*outs, ("dx", "copy", "dgamma", "dbeta", "dsum")):
+        _close(c, a, 1e-6 if nm != "copy" else 8e-3, nm)  # same arithmetic; FMA contraction may differ
+    xr = x.float().requires_grad_(True)
+    torch.nn.functional.layer_norm(xr, (D,), w, b, 1e-6).backward(dy.float())
+    _close(outs[1][0], xr.grad + dres, 1e-5, "ln dx")
+
+
 def test_layer_norm_bwd_compact_rows():
     B, S, D = 3, 5, 768
     x = _rnd(B * S, D, seed=30)

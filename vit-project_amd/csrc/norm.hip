@@ -10,6 +10,7 @@
 #include "common.hpp"
 #include "reduce.hpp"
 #include <stdlib.h>
+#include <type_traits>
 
 constexpr int LN_WAVES = 4;   // rows per block in the forward (one per wave)
 constexpr int LN_SMAX = 32;   // scalar path: D <= 64*32
@@ -270,6 +271,118 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(
 }
 
 
+// Backward, vector form (D = 256 * NV), software-pipelined: a wave issues row r+4's loads (x, dy,
+// the residual gradient, mean / rstd) before row r's arithmetic and stores, so the loads overlap
+// the previous row's stores instead of queueing behind them (vmcnt counts loads and stores in
+// order: the plain loop paid a load and a store latency per row, 8 us per row at the step shape,
+// 4.5 TB/s).  gamma is loaded once per wave.  Same arithmetic, in the same order, as
+// ln_bwd_kernel (the compiler's FMA contraction may differ: equal to rounding).
+template <int NV, typename TX, typename TD> struct LnRow {
+  f32x4 x[NV], r[NV];
+  typename std::conditional<std::is_same<TD, float>::value, f32x4, bf16x4>::type d[NV];
+  float mu, rs;
+};
+
+template <int NV, typename TX, typename TD, typename TC>
+__global__ __launch_bounds__(256) void ln_bwd_pipe_kernel(
+    const TX* __restrict__ x, int64_t ldx, const TD* __restrict__ dy, int64_t lddy,
+    const float* __restrict__ w, const float* __restrict__ mean, const float* __restrict__ rstd,
+    const float* __restrict__ dres, int64_t ldres, float* __restrict__ dx, int64_t lddx,
+    TC* __restrict__ dxc, int64_t ldc, int compact_np, float* __restrict__ part_g,
+    float* __restrict__ part_b, float* __restrict__ part_s, int rows, int D, int rows_per) {
+  constexpr int NP = NV * 4;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  float pg[NP], pb[NP], ps[NP];
+#pragma unroll
+  for (int t = 0; t < NP; ++t) { pg[t] = 0.f; pb[t] = 0.f; ps[t] = 0.f; }
+  f32x4 wg[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) wg[k] = *reinterpret_cast<const f32x4*>(w + col4(lane, k));
+  const int r0 = blockIdx.x * rows_per, r1 = min(rows, r0 + rows_per);
+  using Row = LnRow<NV, TX, TD>;
+  auto load = [&](int row, Row& R) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = col4(lane, k);
+      R.x[k] = ld4<TX>(x + (int64_t)row * ldx + c);
+      if constexpr (std::is_same<TD, float>::value) R.d[k] = *reinterpret_cast<const f32x4*>(dy + (int64_t)row * lddy + c);
+      else R.d[k] = *reinterpret_cast<const bf16x4*>(dy + (int64_t)row * lddy + c);
+      R.r[k] = dres ? *reinterpret_cast<const f32x4*>(dres + (int64_t)row * ldres + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    R.mu = mean[row];
+    R.rs = rstd[row];
+  };
+  auto process = [&](int row, const Row& R) {
+    const float mu = R.mu, rs = R.rs;
+    f32x4 xh[NV], g[NV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      f32x4 dv;
+      if constexpr (std::is_same<TD, float>::value) dv = R.d[k];
+      else dv = f32x4{(float)R.d[k][0], (float)R.d[k][1], (float)R.d[k][2], (float)R.d[k][3]};
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        xh[k][t] = (R.x[k][t] - mu) * rs;
+        g[k][t] = dv[t] * wg[k][t];
+        s1 += g[k][t];
+        s2 += g[k][t] * xh[k][t];
+        pg[k * 4 + t] += dv[t] * xh[k][t];
+        pb[k * 4 + t] += dv[t];
+      }
+    }
+    s1 = wave_sum(s1) / D;
+    s2 = wave_sum(s2) / D;
+    int64_t orow = row;
+    const bool keep = (dxc != nullptr) && copy_row(row, compact_np, orow);
+    float* dxr = dx + (int64_t)row * lddx;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int c = col4(lane, k);
+      f32x4 o;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) o[t] = rs * (g[k][t] - s1 - xh[k][t] * s2);
+      if (dres) o += R.r[k];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) ps[k * 4 + t] += o[t];
+      *reinterpret_cast<f32x4*>(dxr + c) = o;
+      if (keep) st4<TC>(dxc + orow * ldc + c, o);
+    }
+  };
+  // two row buffers, alternated by a 2x unrolled loop (no register copies)
+  Row A, B;
+  int row = r0 + wv;
+  if (row < r1) load(row, A);
+  while (row < r1) {
+    if (row + LN_WAVES < r1) load(row + LN_WAVES, B);
+    process(row, A);
+    row += LN_WAVES;
+    if (row >= r1) break;
+    if (row + LN_WAVES < r1) load(row + LN_WAVES, A);
+    process(row, B);
+    row += LN_WAVES;
+  }
+  if (!part_g && !part_s) return;
+  __shared__ float redv[LN_WAVES][NP][64];
+  auto flush = [&](const float (&p)[NP], float* out) {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) redv[wv][k][lane] = p[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = wv; k < NP; k += LN_WAVES) {
+      const float v = (redv[0][k][lane] + redv[1][k][lane]) + (redv[2][k][lane] + redv[3][k][lane]);
+      out[(int64_t)blockIdx.x * D + col4(lane, k >> 2) + (k & 3)] = v;
+    }
+    __syncthreads();
+  };
+  if (part_g) {
+    flush(pg, part_g);
+    flush(pb, part_b);
+  }
+  if (part_s) flush(ps, part_s);
+}
+
+
 template <typename TX, typename TY>
 static void launch_fwd(int nv, dim3 grid, hipStream_t s, const void* x, int64_t ldx, void* y, int64_t ldy,
                        const float* w, const float* b, float* mean, float* rstd, int rows, int D, float eps) {
@@ -286,17 +399,21 @@ static void launch_fwd(int nv, dim3 grid, hipStream_t s, const void* x, int64_t 
 #undef F
 }
 
+static int g_ln_pipe = -1;  // VIT_LN_BWD_PIPE / vit_layer_norm_bwd_variant: 1 pipelined (default), 0 plain loop
+
 template <typename TX, typename TD, typename TC>
 static void launch_bwd(int nv, int nblk, hipStream_t s, const void* x, int64_t ldx, const void* dy, int64_t lddy,
                        const float* w, const float* mean, const float* rstd, const float* dres, int64_t ldres,
                        float* dx, int64_t lddx, void* dxc, int64_t ldc, int compact_np, float* pg, float* pb,
                        float* ps, int rows, int D, int rows_per) {
-#define B(NV) hipLaunchKernelGGL((ln_bwd_kernel<NV, TX, TD, TC>), dim3(nblk), dim3(64 * LN_WAVES), 0, s, (const TX*)x, ldx, \
+#define B(K, NV) hipLaunchKernelGGL((K<NV, TX, TD, TC>), dim3(nblk), dim3(64 * LN_WAVES), 0, s, (const TX*)x, ldx, \
                                  (const TD*)dy, lddy, w, mean, rstd, dres, ldres, dx, lddx, (TC*)dxc, ldc, compact_np, pg, pb, ps, rows, D, rows_per)
+  if (g_ln_pipe < 0) { const char* v = getenv("VIT_LN_BWD_PIPE"); g_ln_pipe = v ? atoi(v) : 1; }
+  const int pipe = g_ln_pipe;
   switch (nv) {
-    case 3: B(3); break;
-    case 4: B(4); break;
-    default: B(0); break;
+    case 3: if (pipe) B(ln_bwd_pipe_kernel, 3); else B(ln_bwd_kernel, 3); break;
+    case 4: if (pipe) B(ln_bwd_pipe_kernel, 4); else B(ln_bwd_kernel, 4); break;
+    default: B(ln_bwd_kernel, 0); break;
   }
 #undef B
 }
@@ -365,6 +482,9 @@ int vit_add_layer_norm_fwd(int dtype_r, int dtype_y, int rows, int D, const floa
 // dgamma/dbeta and dsum = column sums of dx (the bias gradient of the Linear that
 // produced the LayerNorm's residual input) may each be null; `partial` must hold
 // vit_layer_norm_bwd_partial_floats(rows, D) floats when any of them is requested.
+// Tuning hook: 1 = the software-pipelined vector backward (default), 0 = the plain row loop.
+int vit_layer_norm_bwd_variant(int v) { g_ln_pipe = v; return 0; }
+
 int vit_layer_norm_bwd_blocks(int rows) { return (rows + ln_bwd_rows() - 1) / ln_bwd_rows(); }
 
 int vit_layer_norm_bwd_partial_floats(int rows, int D) {

@@ -50,6 +50,7 @@ SIGNATURES = {
                            i32, vp, vp, vp, vp, i64, i32, vp],
     "vit_layer_norm_bwd_partial_floats": [i32, i32],
     "vit_layer_norm_bwd_blocks": [i32],
+    "vit_layer_norm_bwd_variant": [i32],
     "vit_sdpa_fwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, f32, i32, vp],
     "vit_sdpa_fwd_fp8": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, f32, i32, vp],
     "vit_sdpa_bwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, f32, i32, vp, vp, i64, vp],
