@@ -549,38 +549,42 @@ __device__ __forceinline__ bf16x8 frag_asm(uint32_t img, int s, int kk, int lane
   }
 }
 
-// Blocked CR image (gemm_tile / pp_tile; VIT_CR_BLOCKED): one 1-KiB piece per (32-row k-block kb,
-// 16-column fragment s) at piece kb * (ROWS / 16) + s; inside a piece, k-row rr's 16 columns (32 B)
-// sit in slot cr_sigma(rr).  A fragment read is then a lane-constant address plus an instruction
-// immediate (piece * 1 KiB): no per-read address arithmetic.  The slot permutation makes each
-// ds_read_b64_tr_b16 lane group (k-rows {0-3, 8-11} + 16h, or +4) cover all 64 banks once.
-#ifndef VIT_CR_BLOCKED
-#define VIT_CR_BLOCKED 1
-#endif
-__device__ __forceinline__ int cr_sigma(int r) { return r ^ (((r >> 3) & 1) << 2); }
-// byte offset, inside a piece, of this lane's 8 B of the lo (hi = 0) / hi (hi = 1) transposed read
-__device__ __forceinline__ uint32_t crb_lane(int lane, int hi) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  return (uint32_t)(32 * cr_sigma(8 * g + q + 4 * hi) + 8 * p);
-}
+// transposed 8-B LDS read with a compile-time byte offset in the instruction's offset field
 template <int OFF> __device__ __forceinline__ bf16x4 asm_read_tr_off(uint32_t a) {
   static_assert(OFF >= 0 && OFF < 65536, "ds_read offset field");
   i32x2 v;
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
   return __builtin_bit_cast(bf16x4, v);
 }
-// fragment PIECE (kb * ROWS/16 + s) of a blocked CR image: lo / hi = image base + crb_lane(lane, 0 / 1)
-template <int PIECE> __device__ __forceinline__ bf16x8 frag_crb(uint32_t lo, uint32_t hi) {
-  return cat4(asm_read_tr_off<PIECE * 1024>(lo), asm_read_tr_off<PIECE * 1024>(hi));
-}
-// per-lane source element offset (row-major operand, ld elements per row) of piece t of a blocked
-// CR image of ROWS columns starting at column row0 (< lim), k-rows from r0
+// Half-blocked CR image (gemm_tile, pp_tile; VIT_CR_HB=0 restores the swizzled rows of stage/frag):
+// one 1-KiB piece per (16-row k-block, 32-column fragment pair) -- the piece one global_load_lds
+// fills, reading 16 rows x 64 contiguous bytes like the RC staging.  Inside a piece k-row rr owns
+// 64 B; fragment h (0 / 1) of the pair sits in 32-B half h ^ (rr >> 3 & 1), which puts each
+// transposed read's 32-lane group (k-rows {0-3, 8-11} or {4-7, 12-15}) on all 64 banks once.  A
+// fragment read is a lane base (one per fragment parity) plus an immediate (pair, k-substep): no
+// per-read address arithmetic, which the swizzled-row image needed (its XOR mixes the fragment
+// index with the lane's row).
+#ifndef VIT_CR_HB
+#define VIT_CR_HB 1
+#endif
 template <int ROWS>
-__device__ __forceinline__ int64_t crb_src(int t, int lane, int64_t ld, int row0, int lim) {
-  constexpr int FR = ROWS / 16;
-  const int kb = t / FR, s = t - kb * FR;
-  const int rr = kb * 32 + cr_sigma(lane >> 1);
-  return (int64_t)rr * ld + min(row0 + s * 16 + (lane & 1) * 8, lim - 8);
+__device__ __forceinline__ int64_t crh_src(int t, int lane, int64_t ld, int row0, int lim) {
+  constexpr int FP = ROWS / 32;  // fragment pairs per 16-row k-block
+  const int kb = t / FP, s2 = t - kb * FP;
+  const int rr = lane >> 2, h = ((lane >> 1) & 1) ^ ((rr >> 3) & 1);
+  return (int64_t)(kb * 16 + rr) * ld + min(row0 + s2 * 32 + h * 16 + (lane & 1) * 8, lim - 8);
+}
+// byte offset of this lane's 8 B (lo = 0 / hi = 1 read) of a fragment with parity h, k-substep 0
+template <int ROWS> __device__ __forceinline__ uint32_t crh_lane(int lane, int hi, int h) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const int rr = 8 * (g & 1) + q + 4 * hi;
+  return (uint32_t)((g >> 1) * (ROWS / 32) * 1024 + 64 * rr + 32 * (h ^ ((rr >> 3) & 1)) + 8 * p);
+}
+// fragment S (relative to an even first fragment folded into the bases) at k-substep KK
+template <int ROWS, int KK, int S>
+__device__ __forceinline__ bf16x8 frag_crh(const uint32_t (&base)[2][2], uint32_t cur) {
+  constexpr int OFF = (2 * KK * (ROWS / 32) + S / 2) * 1024;
+  return cat4(asm_read_tr_off<OFF>(cur + base[0][S & 1]), asm_read_tr_off<OFF>(cur + base[1][S & 1]));
 }
 
 __device__ __forceinline__ void lgkm_wait0() {
@@ -636,9 +640,6 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
                                           int64_t ldq, int M, int N, int R, int r_chunk, const Epi& e, int w,
                                           char* smem) {
   constexpr int S = C::STAGES, BM = C::BM, BN = C::BN, BK = C::BK;
-  // blocked CR images for the weight gradient (CR x CR: +10-17 % standalone); the input gradient's
-  // CR weight operand keeps the swizzled rows (its blocked form measured 1-6 % slower)
-  constexpr bool CRB = VIT_CR_BLOCKED && PL == LAY_CR && QL == LAY_CR;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tiles_j = (N + BN - 1) / BN, tiles_i = (M + BM - 1) / BM;
@@ -671,8 +672,8 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
         const int row = t * RPI + lane / CPR;
         const int c = (lane % CPR) ^ rc_sw<BK>(row);
         off[u] = (uint32_t)((int64_t)min(row0 + row, lim - 1) * ld * 2 + c * 16);
-      } else if constexpr (CRB) {
-        off[u] = (uint32_t)(crb_src<ROWS>(t, lane, ld, row0, lim) * 2);
+      } else if constexpr (VIT_CR_HB) {
+        off[u] = (uint32_t)(crh_src<ROWS>(t, lane, ld, row0, lim) * 2);
       } else {
         constexpr int CPR = ROWS / 8, RPI = 64 / CPR;
         const int r = t * RPI + lane / CPR;
@@ -722,13 +723,14 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
   // timing experiments (vit_gemm_variant(v + 100 * bits)): bit 1 drops the ring loads, bit 2 the
   // per-k-step barrier -- the main loop's ceiling without the memory system / the workgroup sync
   const bool dbg_noload = e.dbg & 1, dbg_nobar = e.dbg & 2;
-  // blocked CR images: lane bases of the lo / hi transposed reads, this wave's first fragment folded in
-  uint32_t crb_p[2], crb_q[2];
+  uint32_t crh_p[2][2], crh_q[2][2];  // half-blocked: [lo / hi][fragment parity], first fragment pair folded in
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    crb_p[h] = crb_lane(lane, h) + (uint32_t)(wi * C::AI * 1024);
-    crb_q[h] = C::PIMG + crb_lane(lane, h) + (uint32_t)(wj * C::AJ * 1024);
-  }
+  for (int lh = 0; lh < 2; ++lh)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      crh_p[lh][h] = crh_lane<BM>(lane, lh, h) + (uint32_t)(wi * C::AI / 2 * 1024);
+      crh_q[lh][h] = C::PIMG + crh_lane<BN>(lane, lh, h) + (uint32_t)(wj * C::AJ / 2 * 1024);
+    }
   if (nk > 0) {
 #pragma unroll
     for (int k = 0; k < S - 1; ++k)
@@ -750,11 +752,10 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
               constexpr int b = decltype(bI)::value;
               qf[b] = asm_read128_off<b * 16 * BK * 2>(qa);
             });
-          } else if constexpr (CRB) {  // piece kk * BN/16 + wj * AJ + b (wj folded into crb_q)
-            const uint32_t lo = cur + crb_q[0], hi = cur + crb_q[1];
+          } else if constexpr (VIT_CR_HB) {
             Unroll<C::AJ>::run([&](auto bI) {
               constexpr int b = decltype(bI)::value;
-              qf[b] = frag_crb<kk * (BN / 16) + b>(lo, hi);
+              qf[b] = frag_crh<BN, kk, b>(crh_q, cur);
             });
           } else {
 #pragma unroll
@@ -766,11 +767,10 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
               constexpr int a = decltype(aI)::value;
               pf[a] = asm_read128_off<a * 16 * BK * 2>(pa);
             });
-          } else if constexpr (CRB) {
-            const uint32_t lo = cur + crb_p[0], hi = cur + crb_p[1];
+          } else if constexpr (VIT_CR_HB) {
             Unroll<C::AI>::run([&](auto aI) {
               constexpr int a = decltype(aI)::value;
-              pf[a] = frag_crb<kk * (BM / 16) + a>(lo, hi);
+              pf[a] = frag_crh<BM, kk, a>(crh_p, cur);
             });
           } else {
 #pragma unroll
@@ -782,7 +782,7 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
       }
     } else {
       static_assert(C::KS == 1, "register double-buffering is built for BK = 32");
-      static_assert(!CRB, "load_frags reads the swizzled CR image");
+      static_assert(!(VIT_CR_HB && (PL == LAY_CR || QL == LAY_CR)), "load_frags reads the swizzled CR image");
       // step k: make stage k+1 readable, refill slot k%S with stage k+S-1... (ring of S, S-1 ahead)
       auto step = [&](int k, const bf16x8 (&pc)[C::AI], const bf16x8 (&qc)[C::AJ], bf16x8 (&pn)[C::AI],
                       bf16x8 (&qn)[C::AJ]) {
@@ -909,7 +909,7 @@ __device__ __forceinline__ void pp_tile(const bf16* __restrict__ P, int64_t ldp,
                                         int64_t ldq, int M, int N, int R, int r_chunk, const Epi& e, int w,
                                         char* smem) {
   using C = PP<S>;
-  constexpr bool CRB = VIT_CR_BLOCKED && PL == LAY_CR && QL == LAY_CR;  // blocked CR images (weight gradient)
+  constexpr bool CRH = VIT_CR_HB && PL == LAY_CR && QL == LAY_CR;  // half-blocked CR images (weight gradient)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = wave >> 2, wj = wave & 3;
@@ -955,8 +955,8 @@ __device__ __forceinline__ void pp_tile(const bf16* __restrict__ P, int64_t ldp,
           const int c = (lane % 4) ^ rc_sw<32>(row);
           src[u] = base + (int64_t)min(row0 + row, lim - 1) * ld + rb + c * 8;
           step = 32;
-        } else if constexpr (CRB) {
-          src[u] = base + (int64_t)rb * ld + crb_src<256>(t, lane, ld, row0, lim);
+        } else if constexpr (CRH) {
+          src[u] = base + (int64_t)rb * ld + crh_src<256>(t, lane, ld, row0, lim);
           step = 32 * ld;
         } else {
           const int r = t * 2 + lane / 32;
@@ -985,33 +985,32 @@ __device__ __forceinline__ void pp_tile(const bf16* __restrict__ P, int64_t ldp,
   };
   const bool dbg_noload = e.dbg & 1, dbg_nobar = e.dbg & 2;
   auto bar = [&]() { if (!dbg_nobar) lds_barrier(); };
-  uint32_t crb_p[2], crb_q[2];  // blocked CR images: lane bases, this wave's first fragment folded in
+  uint32_t crh_p[2][2], crh_q[2][2];  // half-blocked: [lo / hi][fragment parity]
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    crb_p[h] = crb_lane(lane, h) + (uint32_t)(grp * 8 * 1024);
-    crb_q[h] = C::PIMG + crb_lane(lane, h) + (uint32_t)(wj * 4 * 1024);
-  }
+  for (int lh = 0; lh < 2; ++lh)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      crh_p[lh][h] = crh_lane<256>(lane, lh, h) + (uint32_t)(grp * 4 * 1024);
+      crh_q[lh][h] = C::PIMG + crh_lane<256>(lane, lh, h) + (uint32_t)(wj * 2 * 1024);
+    }
   // one k-tile = two phases {reads} barrier {16 MFMA} barrier; the next tile's loads are
   // issued in the second read phase, where the partner wave's MFMAs cover their issue
   auto tile = [&](int t, bf16x8 (&qf)[4], bf16x8 (&p0)[4], bf16x8 (&p1)[4]) {
     const uint32_t cur = lds_addr(smem + (t % S) * C::STAGE);
     const bool more = t + S - 1 < nk && !dbg_noload;
-    // blocked CR images: fragment f = piece f, one lane address per half plus an immediate
-    const uint32_t plo = cur + crb_p[0], phi = cur + crb_p[1];
-    if constexpr (CRB) {
-      const uint32_t lo = cur + crb_q[0], hi = cur + crb_q[1];
+    if constexpr (CRH) {
       Unroll<4>::run([&](auto bI) {
         constexpr int b = decltype(bI)::value;
-        qf[b] = frag_crb<b>(lo, hi);
+        qf[b] = frag_crh<256, 0, b>(crh_q, cur);
       });
     } else {
 #pragma unroll
       for (int b = 0; b < 4; ++b) qf[b] = frag_asm<QL, 256, 32>(cur + C::PIMG, wj * 4 + b, 0, lane);
     }
-    if constexpr (CRB) {
+    if constexpr (CRH) {
       Unroll<4>::run([&](auto aI) {
         constexpr int a = decltype(aI)::value;
-        p0[a] = frag_crb<a>(plo, phi);
+        p0[a] = frag_crh<256, 0, a>(crh_p, cur);
       });
     } else {
 #pragma unroll
@@ -1028,10 +1027,10 @@ __device__ __forceinline__ void pp_tile(const bf16* __restrict__ P, int64_t ldp,
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
     bar();
-    if constexpr (CRB) {
+    if constexpr (CRH) {
       Unroll<4>::run([&](auto aI) {
         constexpr int a = decltype(aI)::value;
-        p1[a] = frag_crb<4 + a>(plo, phi);
+        p1[a] = frag_crh<256, 0, 4 + a>(crh_p, cur);
       });
     } else {
 #pragma unroll
