@@ -379,6 +379,61 @@ __device__ __forceinline__ void epilogue_staged(const Epi& e, const f32x4 (&acc)
   }
 }
 
+// GELU pair (bias + act' / act) through a bf16 LDS image of the whole tile: the pair is computed from
+// the pre-activation rounded to bf16 anyway, so every wave writes bf16(acc + bias) at once (one
+// barrier, half the bytes of the f32 band-by-band staging) and the workgroup then sweeps all BM rows
+// row-contiguously (16-B loads / stores).  Bit-identical to epilogue_staged.
+#ifndef VIT_PAIR16
+#define VIT_PAIR16 1
+#endif
+template <class C> struct Pair16 {
+  static constexpr int PITCH = C::BN * 2 + 16;  // 16-B row pad: a fragment write's 16 rows hit distinct banks
+  static constexpr int BYTES = C::BM * PITCH;
+};
+template <class C, int EPI>
+__device__ __forceinline__ void epilogue_pair16(const Epi& e, const f32x4 (&acc)[C::AI][C::AJ], char* smem, int i0,
+                                                int j0, int wi, int wj, int lane, int M, int N) {
+  constexpr int PITCH = Pair16<C>::PITCH, CPR = C::BN / 8, RL = C::THREADS / CPR;
+  static_assert(C::THREADS % CPR == 0, "sweep shape");
+  const int tid = threadIdx.x, g = lane >> 4;
+  __syncthreads();  // every wave's main-loop fragment reads are done
+#pragma unroll
+  for (int b = 0; b < C::AJ; ++b) {
+    const int col = wj * C::WN + b * 16 + 4 * g;
+    const f32x4 bias4 = (e.bias && j0 + col < N) ? *reinterpret_cast<const f32x4*>(e.bias + j0 + col)
+                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int a = 0; a < C::AI; ++a) {
+      const f32x4 v = acc[a][b] + bias4;
+      const bf16x4 pv = {(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(smem + (wi * C::WM + a * 16 + (lane & 15)) * PITCH + col * 2) = pv;
+    }
+  }
+  __syncthreads();
+  const int c = tid % CPR, j = j0 + c * 8;
+  for (int r = tid / CPR; r < C::BM; r += RL) {
+    const int i = i0 + r;
+    const bf16x8 x = *reinterpret_cast<const bf16x8*>(smem + r * PITCH + c * 16);
+    if (i < M && j < N) {
+      if constexpr (EPI == EPI_STORE) {
+        *reinterpret_cast<bf16x8*>((bf16*)e.C + (int64_t)i * e.ldc + j) = x;
+      } else {
+        VecF<8> av, dv;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float ga, gd;
+          if constexpr (EPI == EPI_BIAS_GELU) gelu_fast_both((float)x[q], ga, gd);
+          else quick_gelu_both((float)x[q], ga, gd);
+          av.q[q >> 2][q & 3] = ga;
+          dv.q[q >> 2][q & 3] = gd;
+        }
+        vstore<bf16, 8>((bf16*)e.C + (int64_t)i * e.ldc + j, dv);
+        vstore<bf16, 8>((bf16*)e.aux_out + (int64_t)i * e.ldc + j, av);
+      }
+    }
+  }
+}
+
 // Scalar form for the generic kernel (ragged edges).
 template <int EPI, typename TO, typename TA>
 __device__ __forceinline__ void epi1(const Epi& e, int i, int j, float v) {
@@ -826,6 +881,14 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
                                      (C::EPS == 1 && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU ||
                                                       EPI == EPI_BIAS_QGELU || EPI == EPI_GELU_BWD ||
                                                       EPI == EPI_QGELU_BWD)))) {
+    if constexpr (EPI == EPI_STORE && C::EPS == 0 &&
+                  Pair16<C>::BYTES <= (C::LDS > EpiLds<C, TO>::BYTES ? C::LDS : EpiLds<C, TO>::BYTES)) {
+      // timing experiment (dbg 256): the plain bf16 store through the bf16 LDS image of the tile
+      if ((e.dbg & 256) && !e.csum && N % 8 == 0) {
+        epilogue_pair16<C, EPI>(e, acc, smem, i0, j0, wi, wj, lane, M, N);
+        return;
+      }
+    }
     if (!(e.dbg & (8 | 64)) && N % 32 == 0) {
       epilogue_swap<C, EPI, TO, TA>(e, acc, i0, j0, wi, wj, lane, M, N);
       return;
@@ -835,6 +898,13 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
                                                     EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD)) {
     if ((e.dbg & 16) && N % 32 == 0) {  // timing experiment: the fragment (permlane16) epilogue on any tile
       epilogue_swap<C, EPI, TO, TA>(e, acc, i0, j0, wi, wj, lane, M, N);
+      return;
+    }
+  }
+  if constexpr (sizeof(TO) == 2 && C::EPS == 0 && (EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU) &&
+                Pair16<C>::BYTES <= (C::LDS > EpiLds<C, TO>::BYTES ? C::LDS : EpiLds<C, TO>::BYTES)) {
+    if (VIT_PAIR16 && !e.csum && !(e.dbg & (8 | 128)) && N % 8 == 0) {  // dbg 128: the f32 band staging (A/B)
+      epilogue_pair16<C, EPI>(e, acc, smem, i0, j0, wi, wj, lane, M, N);
       return;
     }
   }
