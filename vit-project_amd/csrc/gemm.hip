@@ -386,6 +386,9 @@ __device__ __forceinline__ void epilogue_staged(const Epi& e, const f32x4 (&acc)
 #ifndef VIT_PAIR16
 #define VIT_PAIR16 1
 #endif
+#ifndef VIT_PLAIN16
+#define VIT_PLAIN16 1
+#endif
 template <class C> struct Pair16 {
   static constexpr int PITCH = C::BN * 2 + 16;  // 16-B row pad: a fragment write's 16 rows hit distinct banks
   static constexpr int BYTES = C::BM * PITCH;
@@ -881,10 +884,12 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
                                      (C::EPS == 1 && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU ||
                                                       EPI == EPI_BIAS_QGELU || EPI == EPI_GELU_BWD ||
                                                       EPI == EPI_QGELU_BWD)))) {
-    if constexpr (EPI == EPI_STORE && C::EPS == 0 &&
+    if constexpr (EPI == EPI_STORE && C::EPS == 0 && C::BM == 256 && C::BN == 256 &&
                   Pair16<C>::BYTES <= (C::LDS > EpiLds<C, TO>::BYTES ? C::LDS : EpiLds<C, TO>::BYTES)) {
-      // timing experiment (dbg 256): the plain bf16 store through the bf16 LDS image of the tile
-      if ((e.dbg & 256) && !e.csum && N % 8 == 0) {
+      // the 256x256 tile: the plain bf16 store through the bf16 LDS image of the tile as well (+1-4 %
+      // standalone over the fragment stores, profiles/r03/gemm_plain_store_bf16_stage_sweep.jsonl);
+      // dbg 256 forces the fragment stores (A/B)
+      if (VIT_PLAIN16 && !(e.dbg & (8 | 64 | 256)) && !e.csum && N % 8 == 0) {
         epilogue_pair16<C, EPI>(e, acc, smem, i0, j0, wi, wj, lane, M, N);
         return;
       }
