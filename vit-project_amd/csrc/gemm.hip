@@ -24,6 +24,16 @@
 #include <type_traits>
 
 enum { LAY_RC = 0, LAY_CR = 1 };
+// build-time switches of the bf16 epilogue forms (A/B builds: -DVIT_PAIR16=0 etc.)
+#ifndef VIT_PAIR16
+#define VIT_PAIR16 1
+#endif
+#ifndef VIT_PLAIN16
+#define VIT_PLAIN16 1
+#endif
+#ifndef VIT_GBWD_PREFETCH
+#define VIT_GBWD_PREFETCH 1
+#endif
 // BIAS_GELU / BIAS_QGELU: C = act'(pre) (what the backward needs), aux_out = act(pre);
 // GELU_BWD / QGELU_BWD: C = acc * aux, aux = that saved act'(pre)  (same for both).
 enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_PATCH = 4,
@@ -327,8 +337,26 @@ __device__ __forceinline__ void epilogue_staged(const Epi& e, const f32x4 (&acc)
   const int c = tid % EL::CPR, r0 = tid / EL::CPR;
   float* red = reinterpret_cast<float*>(smem + EL::STAGE);
   const int j = j0 + c * V;
+  // GELU' input gradient: the act'(pre) rows of band p + 1 (WM/RL rows of 16 B per thread) are loaded
+  // before band p's round, so their HBM latency hides under that round instead of stalling the next
+  constexpr int NPRE = C::WM / EL::RL;
+  constexpr bool PREF = (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) && std::is_same<TA, bf16>::value &&
+                        V == 8 && NPRE <= 4 && VIT_GBWD_PREFETCH;
+  bf16x8 pre[PREF ? NPRE : 1], pre_next[PREF ? NPRE : 1];
+  auto load_pre = [&](int p, bf16x8 (&dst)[PREF ? NPRE : 1]) {
+#pragma unroll
+    for (int u = 0; u < NPRE; ++u) {
+      const int i = i0 + p * C::WM + r0 + u * EL::RL;
+      dst[u] = (i < M && j < N) ? *reinterpret_cast<const bf16x8*>((const bf16*)e.aux + (int64_t)i * e.ld_aux + j)
+                                : bf16x8{};
+    }
+  };
+  if constexpr (PREF) load_pre(0, pre);
 #pragma unroll 1
   for (int p = 0; p < C::WI; ++p) {
+    if constexpr (PREF) {
+      if (p + 1 < C::WI) load_pre(p + 1, pre_next);
+    }
     __syncthreads();  // main-loop fragment reads / the previous band's sweep are done
     if (wi == p) {
 #pragma unroll
@@ -352,7 +380,17 @@ __device__ __forceinline__ void epilogue_staged(const Epi& e, const f32x4 (&acc)
       for (int q = 0; q < V / 4; ++q) v.q[q] = *reinterpret_cast<const f32x4*>(src + 4 * q);
       const int i = ib + r;
       if (i < M && j < N) {
-        epi_vec<EPI, TO, TA, V>(e, i, j, v, z);
+        if constexpr (PREF) {  // epi_vec's GELU' branch, with the prefetched act' row
+          bf16x8 d8 = pre[0];
+#pragma unroll
+          for (int u = 1; u < NPRE; ++u)
+            if (u == (r - r0) / EL::RL) d8 = pre[u];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) v.q[q >> 2][q & 3] *= (float)d8[q];
+          vstore<TO, V>((TO*)e.C + (int64_t)i * e.ldc + j, v);
+        } else {
+          epi_vec<EPI, TO, TA, V>(e, i, j, v, z);
+        }
         if (e.csum) {
 #pragma unroll
           for (int q = 0; q < V / 4; ++q) cs.q[q] += v.q[q];
@@ -376,6 +414,10 @@ __device__ __forceinline__ void epilogue_staged(const Epi& e, const f32x4 (&acc)
         __syncthreads();
       }
     }
+    if constexpr (PREF) {
+#pragma unroll
+      for (int u = 0; u < NPRE; ++u) pre[u] = pre_next[u];
+    }
   }
 }
 
@@ -383,12 +425,6 @@ __device__ __forceinline__ void epilogue_staged(const Epi& e, const f32x4 (&acc)
 // the pre-activation rounded to bf16 anyway, so every wave writes bf16(acc + bias) at once (one
 // barrier, half the bytes of the f32 band-by-band staging) and the workgroup then sweeps all BM rows
 // row-contiguously (16-B loads / stores).  Bit-identical to epilogue_staged.
-#ifndef VIT_PAIR16
-#define VIT_PAIR16 1
-#endif
-#ifndef VIT_PLAIN16
-#define VIT_PLAIN16 1
-#endif
 template <class C> struct Pair16 {
   static constexpr int PITCH = C::BN * 2 + 16;  // 16-B row pad: a fragment write's 16 rows hit distinct banks
   static constexpr int BYTES = C::BM * PITCH;
