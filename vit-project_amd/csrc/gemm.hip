@@ -534,7 +534,7 @@ template <int BM_, int BN_, int BK_, int WI_, int WJ_, int S_, bool DB_, int OCC
 // r-contiguous image, BK=32: 64-B rows, chunk c at row*64 + ((c ^ h(row)) << 4),
 // h(row) = (row & 1) | ((row >> 1) & 2).  BK=64: 128-B rows, chunk c at
 // row*128 + ((c ^ ((row >> 1) & 7)) << 4).  Both conflict-free for the 16x16x32
-// ds_read_b128 fragment pattern (tools/lds_banks.py).
+// ds_read_b128 fragment pattern (tests/test_lds_layouts.py).
 template <int BK> __device__ __forceinline__ int rc_sw(int row) {
   if constexpr (BK == 32) return (row & 1) | ((row >> 1) & 2);
   else return (row >> 1) & 7;
