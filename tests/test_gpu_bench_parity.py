@@ -12,6 +12,10 @@ VIT_FWD_HALF_DELTA = 3B/64, model.fwd_split: M = 27 580 / 22 852 token rows, rag
   (b) every parameter gradient of the bs=256 bf16 step against the HIP fp32 path on the same
       batch (the fp32 path is pinned to the golden fixtures at 1e-3 in test_gpu_parity.py):
       per-tensor cosine >= 0.999 and norm within 2 %;
+  (d) the fp32 HIP path that (b) trusts, at the same bs=256 batch, against the oracle itself:
+      all 256 logit rows, the loss and every parameter gradient within 1e-3 relative (north_star),
+      the oracle's gradient accumulated over 16-image chunks (the mean CE is the mean of the
+      chunks' means, so the chunked sum is the bs=256 gradient and the CPU memory stays small);
   (c) a 30-step bs=32 SGD loss trajectory (lr 0.02 = the reference's warm-up epoch-1 LR,
       momentum 0.9, wd 1e-4) in bf16 against the fp32 HIP path: every step within 1 % (a
       0.01-nat floor once the memorised batch's loss nears 0), and the 30-step parameter change
@@ -136,3 +140,40 @@ def test_bf16_loss_trajectory_tracks_f32_30_steps():
         u, v = delta[torch.bfloat16][k].flatten().double(), delta[torch.float32][k].flatten().double()
         cos = torch.nn.functional.cosine_similarity(u, v, dim=0).item()
         assert cos >= 0.99, (k, cos)
+
+
+def test_f32_path_bs256_matches_oracle(batch):
+    """(d): the fp32 HIP path at bs=256 (two-chain forward, ragged M = 27 580 / 22 852 tiles) against
+    the oracle: logits of every image, the loss and all 152 gradients within 1e-3 relative."""
+    import vit_amd
+    p, x, y = batch
+    m = _bench_model(p, torch.float32)
+    m.zero_grad(set_to_none=True)
+    logits = m(x.to(DEV))
+    loss = vit_amd.cross_entropy(logits, y.to(DEV))
+    loss.backward()
+    torch.cuda.synchronize()
+    got = {k: q.grad.detach().float().cpu() for k, q in m.named_parameters()}
+    ref, ref_logits, ref_loss, C = None, [], 0.0, 16
+    for c in range(0, B, C):
+        leaf = {k: v.detach().clone().requires_grad_(True) for k, v in p.items()}
+        lg = R.forward(leaf, x[c:c + C], R.VIT_B16)
+        lc = R.cross_entropy(lg, y[c:c + C])
+        lc.backward()
+        w = C / B
+        ref_loss += w * float(lc.detach())
+        ref_logits.append(lg.detach())
+        gc = {k: v.grad.detach() * w for k, v in leaf.items()}
+        ref = gc if ref is None else {k: ref[k] + gc[k] for k in ref}
+    ref_logits = torch.cat(ref_logits)
+    lerr = (logits.detach().float().cpu() - ref_logits).abs().max().item() / ref_logits.abs().max().item()
+    assert lerr < 1e-3, lerr
+    lv = float(loss.detach())
+    assert abs(lv - ref_loss) < 1e-3 * abs(ref_loss), (lv, ref_loss)
+    assert got.keys() == ref.keys() and len(got) == 152
+    worst = 0.0
+    for k in got:
+        err = (got[k] - ref[k]).abs().max().item() / (ref[k].abs().max().item() + 1e-30)
+        worst = max(worst, err)
+        assert err < 1e-3, (k, err)
+    print("logits rel", lerr, "worst gradient rel", worst)
