@@ -1428,7 +1428,9 @@ static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool per
   else if (o >= 0) v = o;
   else if (wgrad) v = 8;                                                   // wgrad: ping-pong 256x256
   else if (fwd && act_fwd && o_fwd_gelu >= 0) v = o_fwd_gelu;               // forward with the GELU pair
-  else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : (o_fwd_small >= 0 ? o_fwd_small : 2);  // forward
+  else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : (o_fwd_small >= 0 ? o_fwd_small : 5);  // forward
+  // (the N, R < 1536 forwards -- proj, patch embedding -- moved from V2 to V5 in round 3: +0.35 % step,
+  // same-box pairs, bit-identical loss trajectory; VIT_GEMM_FWD_SMALL=2 restores V2)
   else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;                // dgrad (GELU' epilogue: V1, 2 WG/CU)
   (void)M;
   if ((v == 2 || v == 5 || v == 10) && R % 64) v = 1;                       // BK = 64 configurations need 64-row chunks
