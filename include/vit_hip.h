@@ -216,13 +216,14 @@ int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, 
                         float* sdDnT_ws, const float* noise, void* stream);
 /* torch.optim.AdamW step (NEWP:1181, NEWP:1001): tensors {float* p; const float* g; float* exp_avg;
  * float* exp_avg_sq; bf16* shadow (or null); int64 n; const float* coef}[] where coef points at
- * the tensor's {step_size, bc2_sqrt} in device memory: step_size = lr / (1 - beta1^step) and
+ * the tensor's {step_size, bc2_sqrt, decay, 0} in device memory: step_size = lr / (1 - beta1^step),
  * bc2_sqrt = sqrt(1 - beta2^step) for that tensor's own state['step'] (so a load_state_dict
- * resume, NEWP:1189-1195, continues the bias correction).  The table is fixed across steps (only
- * the coefficients change), so a captured graph can replay it; chunks as vit_sgd_step;
- * decay = 1 - lr * weight_decay. */
-int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, float decay, float beta1, float beta2,
-                   float eps, void* stream);
+ * resume, NEWP:1189-1195, continues the bias correction) and decay = 1 - lr * weight_decay of the
+ * tensor's group.  The table is fixed across steps (only the coefficients change), so a captured
+ * graph can replay it under a changing lr; chunks as vit_sgd_step.  (ABI 6: decay moved from a
+ * scalar argument into coef.) */
+int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, float beta1, float beta2, float eps,
+                   void* stream);
 int vit_adamw_tensor_bytes(void);
 
 /* CLIP-HBA forward/loss around the towers (NEWP:287-304 -> clip_model(image, prompts, pos_embedding),

@@ -747,7 +747,9 @@ def test_fused_adamw_matches_torch():
 
 def test_fused_adamw_table_is_static_and_graph_replay_matches_torch():
     """The AdamW tensor table holds pointers and sizes only (its key does not change from step to
-    step: ADVICE r02); a captured step() replayed after prepare_replay() follows torch.AdamW."""
+    step: ADVICE r02); a captured step() replayed after prepare_replay() follows torch.AdamW, also
+    when the lr changes between replays (an lr schedule: the decoupled decay 1 - lr * wd must follow
+    it as the step size does -- ADVICE r03; wd = 0.5 makes a stale decay visible at 1e-6)."""
     from vit_amd.optim import FusedAdamW
     torch.manual_seed(3)
     shapes = [(48, 512), (512,), (3,)]
@@ -756,8 +758,8 @@ def test_fused_adamw_table_is_static_and_graph_replay_matches_torch():
     gdev = [torch.zeros(s, device=DEV) for s in shapes]
     for q, g in zip(qs, gdev):
         q.grad = g
-    ref = torch.optim.AdamW(ps, lr=3e-4, weight_decay=0.01)
-    opt = FusedAdamW(qs, lr=3e-4, weight_decay=0.01)
+    ref = torch.optim.AdamW(ps, lr=3e-4, weight_decay=0.5)
+    opt = FusedAdamW(qs, lr=3e-4, weight_decay=0.5)
     grads = [[torch.randn(s) for s in shapes] for _ in range(6)]
 
     def feed(gs):
@@ -780,7 +782,9 @@ def test_fused_adamw_table_is_static_and_graph_replay_matches_torch():
         with torch.cuda.graph(graph, stream=s):
             opt.step()
     torch.cuda.current_stream().wait_stream(s)
-    for gs in grads[2:]:
+    for i, gs in enumerate(grads[2:]):
+        for o in (ref, opt):
+            o.param_groups[0]["lr"] = 3e-4 * (1 + 10 * i)  # 3e-4, 3.3e-3, 6.3e-3, 9.3e-3
         feed(gs)
         ref.step()
         opt.prepare_replay()

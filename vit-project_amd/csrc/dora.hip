@@ -101,21 +101,22 @@ __global__ __launch_bounds__(256) void dora_bwd_row_kernel(int in, int out, cons
 // step_size = lr / (1 - b1^step) and sqrt(1 - b2^step) are computed per tensor in
 // double on the host from that tensor's own state['step'] (as torch does), so a
 // resumed optimizer (load_state_dict) continues the bias correction where it was.
-// They live in a separate device array (coef = {step_size, bc2_sqrt} of this tensor)
-// refreshed by one copy per step, so the tensor table itself never changes between
-// steps.  The bf16 GEMM shadow of the parameter (if any) is written in the same pass.
+// They live in a separate device array (coef = {step_size, bc2_sqrt, decay, 0} of this
+// tensor, decay = 1 - lr * weight_decay of its group) refreshed by one copy per step, so
+// the tensor table itself never changes between steps and a replayed graph follows an
+// lr schedule in both the step size and the decoupled decay.  The bf16 GEMM shadow of the parameter (if any) is written in the same pass.
 // ---------------------------------------------------------------------------
 struct AdamTensor { float* p; const float* g; float* m; float* v; bf16* shadow; int64_t n; const float* coef; };
 struct AdamChunk { int tensor; int pad; int64_t start; };
 constexpr int ADAM_CHUNK = 4096;
 
 __global__ __launch_bounds__(256) void adamw_kernel(const AdamTensor* __restrict__ ts, const AdamChunk* __restrict__ chunks,
-                                                    float decay, float b1, float b2, float eps) {
+                                                    float b1, float b2, float eps) {
   const AdamChunk ch = chunks[blockIdx.x];
   const AdamTensor t = ts[ch.tensor];
   const float w1 = 1.f - b1, w2 = 1.f - b2;
   const int64_t end = min(t.n, ch.start + ADAM_CHUNK);
-  const float step_size = t.coef[0], bc2_sqrt = t.coef[1];
+  const float step_size = t.coef[0], bc2_sqrt = t.coef[1], decay = t.coef[2];
   for (int64_t i = ch.start + threadIdx.x; i < end; i += 256) {
     float p = __fmul_rn(t.p[i], decay);
     const float g = t.g[i];
@@ -165,13 +166,13 @@ int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, 
                   stream);
 }
 
-// Fused AdamW over a table of AdamTensor {p, g, m, v, shadow, n, coef -> {step_size, bc2_sqrt}};
-// chunks of 4096 elements {tensor, pad, start}; decay = 1 - lr * weight_decay.
-int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, float decay, float beta1, float beta2,
-                   float eps, void* stream) {
+// Fused AdamW over a table of AdamTensor {p, g, m, v, shadow, n, coef -> {step_size, bc2_sqrt, decay, 0}};
+// chunks of 4096 elements {tensor, pad, start}.
+int vit_adamw_step(const void* tensors, const void* chunks, int nchunks, float beta1, float beta2, float eps,
+                   void* stream) {
   if (nchunks <= 0) return 0;
   hipLaunchKernelGGL(adamw_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, (const AdamTensor*)tensors,
-                     (const AdamChunk*)chunks, decay, beta1, beta2, eps);
+                     (const AdamChunk*)chunks, beta1, beta2, eps);
   VIT_CHECK_LAUNCH();
   return 0;
 }

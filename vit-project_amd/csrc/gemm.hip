@@ -1557,15 +1557,21 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
   }
 }
 
-// Stream-K workspaces registered per stream by the host (vit_gemm_streamk_workspace): the cut-tile
-// fragment images (2 x 64 KiB per workgroup) and one ticket counter per workgroup boundary.
-struct SkWs { hipStream_t s; float* part; int64_t part_bytes; int* cnt; int ncnt; };
+// Stream-K workspaces registered per (device, stream) by the host (vit_gemm_streamk_workspace): the
+// cut-tile fragment images (2 x 64 KiB per workgroup) and one ticket counter per workgroup boundary.
+// The device is part of the key: the null stream is handle 0 on every device.
+struct SkWs { int dev; hipStream_t s; float* part; int64_t part_bytes; int* cnt; int ncnt; };
 static SkWs g_sk[32];
 static int g_nsk = 0;
 static int g_sk_mode = -2;  // VIT_GEMM_STREAMK: 0 off, 1 on (default: on where it removes a ragged round), 2 all k-steps shared
+static int stream_device(hipStream_t s) {  // the null stream: the current device
+  hipDevice_t d = -1;
+  return hipStreamGetDevice(s, &d) == hipSuccess ? (int)d : -1;
+}
 static const SkWs* sk_for(hipStream_t s) {
+  const int d = stream_device(s);
   for (int i = 0; i < g_nsk; ++i)
-    if (g_sk[i].s == s) return &g_sk[i];
+    if (g_sk[i].s == s && g_sk[i].dev == d) return &g_sk[i];
   return nullptr;
 }
 // fraction of the last round's workgroup slots a plain launch of `tiles` leaves empty
@@ -1733,23 +1739,24 @@ extern "C" {
 // launch, 0 when even 256 rows do not fit).
 int vit_gemm_rc_chunk_rows(int M, int64_t ld) { return rc_chunk_rows(M, ld); }
 
-// Stream-K workspace for the f32 MFMA GEMMs launched on `stream` (C3's 128.5-row-tile shapes):
-// part >= 2 * CUs * 2 * 128*128 floats, counters >= 2 * CUs ints zero-filled before first use (the
-// kernel leaves them zero).  part == NULL removes the stream's entry.  Without an entry the plain
-// one-tile-per-workgroup launch runs.
+// Stream-K workspace for the f32 MFMA GEMMs launched on `stream` (C3's 128.5-row-tile shapes; the
+// null stream means the current device's): part >= 2 * CUs * 2 * 128*128 floats, counters >= 2 * CUs
+// ints zero-filled before first use (the kernel leaves them zero), both on the stream's device.  part == NULL removes
+// the (device, stream) entry.  Without an entry the plain one-tile-per-workgroup launch runs.
 int vit_gemm_streamk_workspace(void* stream, float* part, int64_t part_bytes, int* counters, int ncounters) {
   hipStream_t s = (hipStream_t)stream;
+  const int d = stream_device(s);
   for (int i = 0; i < g_nsk; ++i)
-    if (g_sk[i].s == s) {
+    if (g_sk[i].s == s && g_sk[i].dev == d) {
       if (part == nullptr) {
         g_sk[i] = g_sk[--g_nsk];
         return 0;
       }
-      g_sk[i] = SkWs{s, part, part_bytes, counters, ncounters};
+      g_sk[i] = SkWs{d, s, part, part_bytes, counters, ncounters};
       return 0;
     }
   if (part == nullptr || g_nsk == 32) return 0;  // a full registry: the stream keeps the plain launch
-  g_sk[g_nsk++] = SkWs{s, part, part_bytes, counters, ncounters};
+  g_sk[g_nsk++] = SkWs{d, s, part, part_bytes, counters, ncounters};
   return 0;
 }
 

@@ -293,6 +293,6 @@ int vit_zero(void* p, int64_t bytes, void* stream) {
   return (int)hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);
 }
 
-int vit_abi_version(void) { return 5; }
+int vit_abi_version(void) { return 6; }
 
 }  // extern "C"

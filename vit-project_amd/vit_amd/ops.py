@@ -48,19 +48,24 @@ def _keep(t: torch.Tensor):
 # GEMMs
 # ----------------------------------------------------------------------------
 
-_SK = {}  # stream handle -> (part, counters) registered with vit_gemm_streamk_workspace
+_SK = {}  # (device index, stream handle) -> (part, counters) registered with vit_gemm_streamk_workspace
 
 
 def _streamk(device):
-    """Register (once per stream) the stream-K workspace the f32 MFMA GEMMs use on the current stream."""
+    """Register (once per (device, stream)) the stream-K workspace the f32 MFMA GEMMs use on the
+    current stream.  Keyed by device too: the null stream has handle 0 on every device.  Under
+    graph capture an unregistered stream stays unregistered (the workspace's zero-fill would be
+    captured, not run, and its memory would come from the graph's pool): the plain launch runs."""
     st = L.stream_ptr(device)
-    if st in _SK:
+    key = (torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device(), st)
+    if key in _SK or torch.cuda.is_current_stream_capturing():
         return
     g = 2 * torch.cuda.get_device_properties(device).multi_processor_count
     part = torch.empty(g * 2 * 128 * 128, dtype=torch.float32, device=device)
     cnt = torch.zeros(g, dtype=torch.int32, device=device)
-    call("vit_gemm_streamk_workspace", st, ptr(part), part.numel() * 4, ptr(cnt), g)
-    _SK[st] = (part, cnt)
+    with torch.cuda.device(key[0]):
+        call("vit_gemm_streamk_workspace", st, ptr(part), part.numel() * 4, ptr(cnt), g)
+    _SK[key] = (part, cnt)
 
 
 def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, resid=None, act_out=None):

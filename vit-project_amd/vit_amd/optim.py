@@ -178,7 +178,7 @@ class FusedAdamW(torch.optim.Optimizer):
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self._mt = {}
-        self._coef = {}   # group index -> device float32 [2 * ntensors]
+        self._coef = {}   # group index -> device float32 [4 * ntensors]
         self._ring = {}   # group index -> [pinned host buffer, event or None] * RING
         self._ring_pos = {}
         self._captured = {}  # group index -> the parameter list a capture recorded
@@ -187,9 +187,11 @@ class FusedAdamW(torch.optim.Optimizer):
         return [p for p in group["params"] if p.grad is not None]
 
     def _advance(self, group, params):
-        """state['step'] += 1 for each tensor; the (lr / bc1, sqrt(bc2)) pairs of the new step."""
+        """state['step'] += 1 for each tensor; the (lr / bc1, sqrt(bc2), 1 - lr * wd, 0) rows of the
+        new step (the decay is per step too, so a replay follows a changed lr in both terms)."""
         lr, (b1, b2) = float(group["lr"]), group["betas"]
-        coef = np.empty(2 * len(params), dtype=np.float32)
+        decay = 1.0 - lr * float(group["weight_decay"])
+        coef = np.zeros(4 * len(params), dtype=np.float32)
         for i, p in enumerate(params):
             st = self.state[p]
             if len(st) == 0:
@@ -198,14 +200,19 @@ class FusedAdamW(torch.optim.Optimizer):
                 st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
             st["step"] += 1
             step = float(st["step"].item())
-            coef[2 * i] = lr / (1.0 - b1 ** step)
-            coef[2 * i + 1] = math.sqrt(1.0 - b2 ** step)
+            coef[4 * i] = lr / (1.0 - b1 ** step)
+            coef[4 * i + 1] = math.sqrt(1.0 - b2 ** step)
+            coef[4 * i + 2] = decay
         return coef
 
-    def _upload(self, gi, coef, dev):
+    def _upload(self, gi, coef, dev, replay=False):
         """One async copy of this step's coefficients into the group's device array, through a
-        ring of pinned buffers (a buffer is rewritten only after its previous copy finished)."""
+        ring of pinned buffers (a buffer is rewritten only after its previous copy finished).
+        ``replay``: the array is the one a captured graph reads, so it must not be reallocated."""
         cd = self._coef.get(gi)
+        if replay and (cd is None or cd.numel() != coef.size or cd.device != dev):
+            raise RuntimeError("FusedAdamW.prepare_replay: the captured coefficient array does not match "
+                               "the captured parameter list; re-capture the graph")
         if cd is None or cd.numel() != coef.size or cd.device != dev:
             cd = self._coef[gi] = torch.empty(coef.size, dtype=torch.float32, device=dev)
             self._ring[gi] = [[torch.empty(coef.size, dtype=torch.float32).pin_memory(), None]
@@ -230,7 +237,7 @@ class FusedAdamW(torch.optim.Optimizer):
         for gi, group in enumerate(self.param_groups):
             params = self._captured.get(gi)
             if params:
-                self._upload(gi, self._advance(group, params), params[0].device)
+                self._upload(gi, self._advance(group, params), params[0].device, replay=True)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -245,14 +252,18 @@ class FusedAdamW(torch.optim.Optimizer):
                 continue
             dev = params[0].device
             L.require_gpu(torch.empty(0, device=dev))
-            lr, (b1, b2), eps, wd = float(group["lr"]), group["betas"], float(group["eps"]), float(group["weight_decay"])
+            (b1, b2), eps = group["betas"], float(group["eps"])
             if capturing:
                 if self._coef.get(gi) is None:
                     raise RuntimeError("FusedAdamW: run one eager step() before capturing (it builds the tensor "
                                        "table and the coefficient buffer); then call prepare_replay() before "
                                        "each replay")
-                self._captured[gi] = params
                 cd = self._coef[gi]
+                if cd.numel() != 4 * len(params):
+                    raise RuntimeError(f"FusedAdamW: capturing {len(params)} tensors with gradients in group {gi}, "
+                                       f"but the last eager step() built the table for {cd.numel() // 4}; run an "
+                                       "eager step with the same parameters first")
+                self._captured[gi] = params
             else:
                 coef = self._advance(group, params)
                 for p in params:
@@ -269,13 +280,13 @@ class FusedAdamW(torch.optim.Optimizer):
                 st = self.state[p]
                 sh = getattr(p, "_vit_shadow", None)
                 entries.append((p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
-                                None if sh is None else sh.data_ptr(), p.numel(), base + 8 * i))
+                                None if sh is None else sh.data_ptr(), p.numel(), base + 16 * i))
                 sizes.append(p.numel())
             mt = self._mt.get(gi)
             if mt is None:
                 mt = self._mt[gi] = _MultiTensor(dev, fields=7)
             mt.build(entries, sizes)
-            call("vit_adamw_step", mt._tdev.data_ptr(), mt._cdev.data_ptr(), mt.nchunks, float(1.0 - lr * wd),
+            call("vit_adamw_step", mt._tdev.data_ptr(), mt._cdev.data_ptr(), mt.nchunks,
                  float(b1), float(b2), eps, L.stream_ptr(dev))
             for p in params:
                 _mark_updated(p)
