@@ -23,7 +23,7 @@
 #include <string.h>
 #include <type_traits>
 
-enum { LAY_RC = 0, LAY_CR = 1 };
+#include "gemm_lds.hpp"
 // build-time switches of the bf16 epilogue forms (A/B builds: -DVIT_PAIR16=0 etc.)
 #ifndef VIT_PAIR16
 #define VIT_PAIR16 1
@@ -531,23 +531,6 @@ template <int BM_, int BN_, int BK_, int WI_, int WJ_, int S_, bool DB_, int OCC
   static_assert(LDS <= 163840, "LDS");
 };
 
-// r-contiguous image, BK=32: 64-B rows, chunk c at row*64 + ((c ^ h(row)) << 4),
-// h(row) = (row & 1) | ((row >> 1) & 2).  BK=64: 128-B rows, chunk c at
-// row*128 + ((c ^ ((row >> 1) & 7)) << 4).  Both conflict-free for the 16x16x32
-// ds_read_b128 fragment pattern (tests/test_lds_layouts.py).
-template <int BK> __device__ __forceinline__ int rc_sw(int row) {
-  if constexpr (BK == 32) return (row & 1) | ((row >> 1) & 2);
-  else return (row >> 1) & 7;
-}
-template <int BK> __device__ __forceinline__ int rc_off(int row, int c) {
-  return row * (BK * 2) + ((c ^ rc_sw<BK>(row)) << 4);
-}
-// r-strided image: BK r-rows x COLS (COLS*2-byte rows), chunk c at
-// r*COLS*2 + (((c & ~15) | ((c & 15) ^ f(r))) << 4), f(r) = ((r&3)<<2)|((r>>2)&3):
-// conflict-free for the two ds_read_b64_tr_b16 of a fragment (rows 8g+q, 8g+4+q).
-__device__ __forceinline__ int cr_f(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
-__device__ __forceinline__ int cr_swz(int c, int r) { return (c & ~15) | ((c & 15) ^ cr_f(r)); }
-template <int COLS> __device__ __forceinline__ int cr_off(int r, int c) { return r * COLS * 2 + (cr_swz(c, r) << 4); }
 
 // Stage a ROWS x BK operand tile into an LDS image; each wave issues G_OP 1-KiB
 // global_load_lds.  Rows (RC) / columns (CR) past `lim` are clamped to valid
@@ -592,123 +575,6 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int s, int kk, int lane)
   }
 }
 
-// Fragment reads as inline asm: the compiler cannot see them as LDS reads, so it
-// does not put an s_waitcnt vmcnt(0) (for the in-flight global_load_lds writes it
-// cannot prove disjoint) in front of them.  The caller orders them: a counted
-// vmcnt + barrier before (data landed), lgkm_wait0() before the first use.
-typedef int i32x4 __attribute__((ext_vector_type(4)));
-typedef int i32x2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-  return (uint32_t)(uintptr_t)LDS_PTR(p);
-}
-__device__ __forceinline__ bf16x8 asm_read128(uint32_t a) {
-  i32x4 v;
-  asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
-  return __builtin_bit_cast(bf16x8, v);
-}
-// the same read with a compile-time byte offset in the instruction's 16-bit offset field: the
-// fragments of one wave differ from each other only by such constants (below), so the loop
-// needs one address VGPR per k-substep instead of one v_add per fragment read
-template <int OFF> __device__ __forceinline__ bf16x8 asm_read128_off(uint32_t a) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds_read offset field");
-  i32x4 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
-  return __builtin_bit_cast(bf16x8, v);
-}
-template <int N> struct Unroll {
-  template <class F> __device__ __forceinline__ static void run(F&& f) {
-    Unroll<N - 1>::run(f);
-    f(std::integral_constant<int, N - 1>{});
-  }
-};
-template <> struct Unroll<0> {
-  template <class F> __device__ __forceinline__ static void run(F&&) {}
-};
-__device__ __forceinline__ bf16x4 asm_read_tr(uint32_t a) {
-  i32x2 v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
-  return __builtin_bit_cast(bf16x4, v);
-}
-template <int LAY, int ROWS, int BK>
-__device__ __forceinline__ bf16x8 frag_asm(uint32_t img, int s, int kk, int lane) {
-  if constexpr (LAY == LAY_RC) {
-    return asm_read128(img + rc_off<BK>(s * 16 + (lane & 15), kk * 4 + (lane >> 4)));
-  } else {
-    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-    const int c = 2 * s + (p >> 1);
-    const int r0 = kk * 32 + 8 * g + q;
-    bf16x4 lo = asm_read_tr(img + cr_off<ROWS>(r0, c) + (p & 1) * 8);
-    bf16x4 hi = asm_read_tr(img + cr_off<ROWS>(r0 + 4, c) + (p & 1) * 8);
-    return cat4(lo, hi);
-  }
-}
-
-// transposed 8-B LDS read with a compile-time byte offset in the instruction's offset field
-template <int OFF> __device__ __forceinline__ bf16x4 asm_read_tr_off(uint32_t a) {
-  static_assert(OFF >= 0 && OFF < 65536, "ds_read offset field");
-  i32x2 v;
-  asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
-  return __builtin_bit_cast(bf16x4, v);
-}
-// Half-blocked CR image (gemm_tile, pp_tile; VIT_CR_HB=0 restores the swizzled rows of stage/frag):
-// one 1-KiB piece per (16-row k-block, 32-column fragment pair) -- the piece one global_load_lds
-// fills, reading 16 rows x 64 contiguous bytes like the RC staging.  Inside a piece k-row rr owns
-// 64 B; fragment h (0 / 1) of the pair sits in 32-B half h ^ (rr >> 3 & 1), which puts each
-// transposed read's 32-lane group (k-rows {0-3, 8-11} or {4-7, 12-15}) on all 64 banks once.  A
-// fragment read is a lane base (one per fragment parity) plus an immediate (pair, k-substep): no
-// per-read address arithmetic, which the swizzled-row image needed (its XOR mixes the fragment
-// index with the lane's row).
-#ifndef VIT_CR_HB
-#define VIT_CR_HB 1
-#endif
-template <int ROWS>
-__device__ __forceinline__ int64_t crh_src(int t, int lane, int64_t ld, int row0, int lim) {
-  constexpr int FP = ROWS / 32;  // fragment pairs per 16-row k-block
-  const int kb = t / FP, s2 = t - kb * FP;
-  const int rr = lane >> 2, h = ((lane >> 1) & 1) ^ ((rr >> 3) & 1);
-  return (int64_t)(kb * 16 + rr) * ld + min(row0 + s2 * 32 + h * 16 + (lane & 1) * 8, lim - 8);
-}
-// byte offset of this lane's 8 B (lo = 0 / hi = 1 read) of a fragment with parity h, k-substep 0
-template <int ROWS> __device__ __forceinline__ uint32_t crh_lane(int lane, int hi, int h) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const int rr = 8 * (g & 1) + q + 4 * hi;
-  return (uint32_t)((g >> 1) * (ROWS / 32) * 1024 + 64 * rr + 32 * (h ^ ((rr >> 3) & 1)) + 8 * p);
-}
-// fragment S (relative to an even first fragment folded into the bases) at k-substep KK
-template <int ROWS, int KK, int S>
-__device__ __forceinline__ bf16x8 frag_crh(const uint32_t (&base)[2][2], uint32_t cur) {
-  constexpr int OFF = (2 * KK * (ROWS / 32) + S / 2) * 1024;
-  return cat4(asm_read_tr_off<OFF>(cur + base[0][S & 1]), asm_read_tr_off<OFF>(cur + base[1][S & 1]));
-}
-
-__device__ __forceinline__ void lgkm_wait0() {
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  // bijective: blocks that share an XCD (bid % 8) get a contiguous range of ids
-  int xcd = bid & 7, q = nwg >> 3, r = nwg & 7, k = bid >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
-}
-
-template <int N> __device__ __forceinline__ void wait_vm() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-// wait until at most n stages (of G loads each) of this wave remain in flight
-template <int G, int S>
-__device__ __forceinline__ void wait_stages(int n) {
-  if constexpr (S >= 6) { if (n >= 5) { wait_vm<5 * G>(); return; } }
-  if constexpr (S >= 5) { if (n >= 4) { wait_vm<4 * G>(); return; } }
-  if constexpr (S >= 4) { if (n >= 3) { wait_vm<3 * G>(); return; } }
-  if constexpr (S >= 3) { if (n >= 2) { wait_vm<2 * G>(); return; } }
-  if (n >= 1) { wait_vm<G>(); return; }
-  wait_vm<0>();
-}
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
 
 // Tile t of a tiles_i x tiles_j grid.  group_m == 0: row-major (consecutive t share a row tile,
 // so the P rows stay in the XCD's L2 while every Q column block streams past).  group_m > 0:
@@ -1778,12 +1644,52 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
                   (hipStream_t)stream, allow_fast != 0);
 }
 
+// The multi-tile deferred-store kernel (gemm_ms.hip) for the bf16 forwards (plain / GELU pair) and the
+// plain bf16 input gradients: VIT_GEMM_MS = bit mask (1 = forwards, 2 = input gradients; 0 = off, A/B),
+// VIT_GEMM_MS_CFG = its configuration (vit_gemm_ms cfg: row tile and store deferral), VIT_GEMM_MS_T =
+// tiles per workgroup (the grid is ceil(tiles / T)); a forced tile variant (vit_gemm_variant, the
+// tuning sweeps) bypasses it.
+extern "C" int vit_gemm_ms(int epi, int wl, int bm, int M, int N, int K, const void* X, int64_t ldx, const void* W,
+                           int64_t ldw, const float* bias, void* C, int64_t ldc, void* C2, int grid, void* stream);
+static int g_ms[3] = {-2, 0, 2};  // class mask, cfg, tiles per workgroup; -2 = not yet read from the environment
+static bool ms_on(int wl) {
+  if (g_ms[0] == -2) {
+    const int on = env_variant("VIT_GEMM_MS"), cfg = env_variant("VIT_GEMM_MS_CFG"), t = env_variant("VIT_GEMM_MS_T");
+    g_ms[0] = on == -1 ? 0 : on;
+    if (cfg >= 0) g_ms[1] = cfg;
+    if (t >= 1) g_ms[2] = t;
+  }
+  return (g_ms[0] >> wl & 1) && g_variant < 0;
+}
+// hipErrorInvalidValue from vit_gemm_ms = shape outside its contract: the caller takes the V* kernels
+static int try_ms(int epi, int wl, int M, int N, int K, const void* X, int64_t ldx, const void* W, int64_t ldw,
+                  const float* bias, void* C, int64_t ldc, void* C2, hipStream_t s) {
+  if (!ms_on(wl)) return (int)hipErrorInvalidValue;
+  const int bm = (g_ms[1] == 1 || g_ms[1] == 2) ? 256 : 192;
+  const int tiles = ((M + bm - 1) / bm) * (N / 256);
+  const int grid = (tiles + g_ms[2] - 1) / g_ms[2];
+  return vit_gemm_ms(epi, wl, g_ms[1], M, N, K, X, ldx, W, ldw, bias, C, ldc, C2, grid, s);
+}
+
+// Tuning hook (A/B runs): the multi-tile kernel's class mask (1 forwards, 2 input gradients), its row tile
+// and tiles per workgroup (-1 keeps one).
+int vit_gemm_ms_config(int on, int cfg, int tiles_per_wg) {
+  (void)ms_on(0);
+  if (on >= 0) g_ms[0] = on;
+  if (cfg >= 0) g_ms[1] = cfg;
+  if (tiles_per_wg >= 1) g_ms[2] = tiles_per_wg;
+  return 0;
+}
+
 // F.linear forward: Y[M,N] = X[M,K] W[N,K]^T + b with a fused epilogue
 //   epi = EPI_STORE (Y out_dtype), EPI_BIAS_GELU / EPI_BIAS_QGELU (Y = act'(pre), act_out = act(pre)),
 //   EPI_RESID (Y f32 = resid + X W^T + b; Y may alias resid).
 int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const void* X, int64_t ldx,
                    const void* W, const float* bias, void* Y, int64_t ldy, const void* resid,
                    void* act_out, void* stream) {
+  if (dtype == VIT_BF16 && out_dtype == VIT_BF16 && (epi == EPI_STORE || epi == EPI_BIAS_GELU) &&
+      try_ms(epi == EPI_BIAS_GELU, 0, M, N, K, X, ldx, W, K, bias, Y, ldy, act_out, (hipStream_t)stream) == 0)
+    return 0;
   Epi e = make_epi();
   e.C = Y; e.ldc = ldy; e.bias = bias; e.aux = resid; e.ld_aux = ldy; e.aux_out = act_out;
   return gemm_any(epi, dtype, out_dtype, LAY_RC, LAY_RC, M, N, K, X, ldx, W, K, 1, e, (hipStream_t)stream);
@@ -1803,6 +1709,9 @@ int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, con
                      const void* W, void* dX, int64_t lddx, const void* pre, float* dbias, float* partial,
                      int64_t partial_floats, int defer_reduce, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (dtype == VIT_BF16 && out_dtype == VIT_BF16 && epi == EPI_STORE && !dbias &&
+      try_ms(0, 1, M, K, N, dY, lddy, W, K, nullptr, dX, lddx, nullptr, s) == 0)
+    return 0;
   Epi e = make_epi();
   e.C = dX; e.ldc = lddx; e.aux = pre; e.ld_aux = lddx;
   const int rows = (M + 63) / 64;
