@@ -203,6 +203,10 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
                  float* delta_ws, float scale, int causal, float* dbias, float* partial, int64_t partial_floats,
                  void* stream);
 int vit_sdpa_bwd_partial_floats(int B, int N, int D);
+/* Tuning hook: the bf16 backward form for N <= 224 (-1 = from VIT_ATTN_BWD_BAND / VIT_ATTN_BWD_SPLIT,
+ * 0 = banded queries (N > 112; opt-in, measured slower), 1 = whole-head fused (the default), 2 = two
+ * kernels).  All forms give bit-identical dq / dk / dv. */
+int vit_sdpa_bwd_variant(int v);
 
 /* torch.nn.functional.cross_entropy(outputs, targets) mean (VIT:140) and its gradient. */
 int vit_cross_entropy_fwd(int B, int C, const float* logits, int64_t ld, const int64_t* target, float* row_lse,

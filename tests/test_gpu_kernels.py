@@ -632,6 +632,36 @@ def test_sdpa_bwd_large_grid(B, H, N, causal):
     assert worst < 3e-2, f"worst (b, h) item rel err {worst}"
 
 
+@pytest.mark.parametrize("N,causal", [(113, False), (150, False), (197, False), (224, False), (197, True),
+                                      (224, True)])
+def test_sdpa_bwd_banded_matches_whole_head(N, causal):
+    """The banded backward (queries streamed in 32-row bands, round 4) against the whole-head fused
+    kernel: dq / dk / dv bit-identical (same MFMA order per output), delta identical, the qkv-bias
+    column sums within fp32 summation-order error; B*H = 300 workgroups (several per CU slot)."""
+    B, H = 25, 12
+    D = H * 64
+    g = torch.Generator(device=DEV).manual_seed(37)
+    qkv = (torch.randn(B * N, 3 * D, device=DEV, generator=g) * 1.5).to(torch.bfloat16)
+    do = torch.randn(B * N, D, device=DEV, generator=g).to(torch.bfloat16)
+    o, lse = ops.sdpa_fwd(qkv, B, H, N, causal=causal)
+    lib = L.lib()
+    outs = []
+    try:
+        for v in (1, 0):
+            lib.vit_sdpa_bwd_variant(v)
+            dbias = torch.empty(3 * D, device=DEV)
+            dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=dbias, causal=causal)
+            delta = ops.workspace("sdpa_delta", B * H * N * 4, qkv.device).view(torch.float32)[:B * H * N].clone()
+            torch.cuda.synchronize()
+            outs.append((dqkv.clone(), dbias.clone(), delta))
+    finally:
+        lib.vit_sdpa_bwd_variant(-1)
+    (d0, b0, l0), (d1, b1, l1) = outs
+    assert torch.equal(d0, d1), (d0.float() - d1.float()).abs().max().item()
+    assert torch.equal(l0, l1)
+    _close(b1, b0, 1e-5, "qkv bias grad (banded vs fused)")
+
+
 @pytest.mark.parametrize("N", [77, 16, 197, 224])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_sdpa_causal_fwd_bwd(N, dtype):

@@ -55,6 +55,7 @@ SIGNATURES = {
     "vit_layer_norm_bwd_variant": [i32],
     "vit_sdpa_fwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, f32, i32, vp],
     "vit_sdpa_fwd_fp8": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, f32, i32, vp],
+    "vit_sdpa_bwd_variant": [i32],
     "vit_sdpa_bwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, f32, i32, vp, vp, i64, vp],
     "vit_sdpa_bwd_partial_floats": [i32, i32, i32],
     "vit_patch_unfold": [i32, i32, i32, i32, i32, i32, vp, vp, vp],
