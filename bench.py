@@ -137,32 +137,51 @@ def cpu_baseline(seconds: float):
                       f"{el:.1f} s, torch CPU {threads} threads (the process's CPU share of {total})"}
 
 
+# the sources the weight-gradient kernel is built from: a committed counter file records their hash
+# (tools/pmc_traffic.py / tools/pmc_step_classes.py --src-sha), so the bench line can say whether the
+# counters it quotes were taken on the kernel that ran
+WGRAD_SOURCES = ("vit-project_amd/csrc/gemm.hip", "vit-project_amd/csrc/gemm_lds.hpp")
+
+
+def wgrad_src_sha():
+    import hashlib
+    h = hashlib.sha256()
+    for f in WGRAD_SOURCES:
+        with open(os.path.join(ROOT, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def _latest_counter_file(pattern):
+    import glob
+    return sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", pattern)), reverse=True)
+
+
 def _pmc_mfma_busy():
     """MFMA-busy fraction of the weight-gradient class from the latest committed step counter
-    passes (profiles/r0N/pmc_step_classes*.json, tools/pmc_step_classes.py), or None."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r0*", "pmc_step_classes*.json")))
-    for f in reversed(files):
+    passes (profiles/r0N/pmc_step_classes*.json, tools/pmc_step_classes.py), its source file and
+    source hash (None when the file predates the hash), or Nones."""
+    for f in _latest_counter_file("pmc_step_classes*.json"):
         try:
             with open(f) as fh:
-                c = json.load(fh)["classes"]["gemm wgrad"]
-            return c.get("mfma_busy"), os.path.relpath(f, ROOT)
+                d = json.load(fh)
+            return d["classes"]["gemm wgrad"].get("mfma_busy"), os.path.relpath(f, ROOT), d.get("src_sha")
         except (OSError, KeyError, ValueError):
             continue
-    return None, None
+    return None, None, None
 
 
 def _pmc_traffic(name):
-    """HBM bytes per launch of a kernel from committed counter passes (tools/pmc_traffic.py;
-    FETCH_SIZE doubled per the gfx950 correction), or None."""
-    for rnd in ("r03", "r02", "r01"):
-        f = os.path.join(ROOT, "profiles", rnd, name)
+    """HBM bytes per launch of a kernel from the latest committed counter passes (tools/pmc_traffic.py;
+    FETCH_SIZE doubled per the gfx950 correction), its file and source hash, or Nones."""
+    for f in _latest_counter_file(name):
         try:
             with open(f) as fh:
-                return int(json.load(fh)["traffic_bytes_per_launch"]), f"profiles/{rnd}/{name}"
+                d = json.load(fh)
+            return int(d["traffic_bytes_per_launch"]), os.path.relpath(f, ROOT), d.get("src_sha")
         except (OSError, KeyError, ValueError):
             continue
-    return None, None
+    return None, None, None
 
 
 # ----------------------------------------------------------------------------
@@ -432,8 +451,9 @@ def main(a):
     value = imgs / el
     ms = el / a.steps * 1e3
     step_tflops = value / world * STEP_FLOP_PER_IMG / 1e12
-    traffic, traffic_src = _pmc_traffic("pmc_traffic_wgrad_pair.json")
-    mfma_busy, busy_src = _pmc_mfma_busy()
+    traffic, traffic_src, traffic_sha = _pmc_traffic("pmc_traffic_wgrad_pair.json")
+    mfma_busy, busy_src, busy_sha = _pmc_mfma_busy()
+    src_sha = wgrad_src_sha()
     if wg is not None:
         roof = {"bound": "mfma", "kernel": "big::pp_kernel2 / pp_kernel (split-K weight-gradient GEMM, 256x256x32 "
                                            "ping-pong; fc2+fc1 and proj+qkv as grouped pairs): every bf16 dW = dY^T X "
@@ -453,7 +473,10 @@ def main(a):
                                 "WRITE_SIZE, rocprofv3 --pmc passes, %s)" % traffic_src,
                 "mfma_busy": mfma_busy,
                 "mfma_busy_unit": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8) of the weight-gradient "
-                                  "launches in the step's counter passes (dispatches serialized; %s)" % busy_src}
+                                  "launches in the step's counter passes (dispatches serialized; %s)" % busy_src,
+                # the counter files record the hash of the kernel sources they were taken on
+                "counters_src_sha": {"kernel_sources": src_sha, "traffic": traffic_sha, "mfma_busy": busy_sha},
+                "counters_match_kernel": traffic_sha == src_sha and busy_sha == src_sha}
     else:
         roof = {"bound": "mfma", "kernel": "big::pp_kernel fc1 weight gradient, standalone",
                 "achieved": round(k_tflops, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",

@@ -138,8 +138,10 @@ def main():
             e["hbm_gbs"] = round(c["bytes"] / (c["time_us"] * 1e3), 1)
         classes[name] = e
     rows = sorted(kernels.values(), key=lambda r: -(r.get("avg_us", 0) * r.get("dispatches", 0)))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import wgrad_src_sha  # the weight-gradient kernel sources these counters were taken on
     res = {"source": d, "program": "tools/step_probe.py (bench step, bs=256 bf16), dispatches serialized by the "
-                                   "counter passes", "kernels": rows, "classes": classes}
+                                   "counter passes", "src_sha": wgrad_src_sha(), "kernels": rows, "classes": classes}
     for r in rows[:24]:
         print(f"{r['label'][:46]:46s} n={r.get('dispatches', 0):4d} {r.get('avg_us', 0):8.1f} us  "
               f"mfma {r.get('mfma_busy', float('nan')):.3f}  clk {r.get('clock_ghz', float('nan')):.2f}  "

@@ -50,6 +50,9 @@ def main():
         res["write_bytes"] = write * 1024
     if fetch is not None and write is not None:
         res["traffic_bytes_per_launch"] = res["fetch_bytes_corrected"] + res["write_bytes"]
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import wgrad_src_sha  # the kernel sources these counters were taken on
+    res["src_sha"] = wgrad_src_sha()
     print(json.dumps(res, indent=1))
     if out:
         with open(out, "w") as fh:

@@ -34,6 +34,12 @@
 #ifndef VIT_GBWD_PREFETCH
 #define VIT_GBWD_PREFETCH 1
 #endif
+#ifndef VIT_SPLIT_ISSUE
+#define VIT_SPLIT_ISSUE 1
+#endif
+#ifndef VIT_SPLIT_ISSUE1
+#define VIT_SPLIT_ISSUE1 1
+#endif
 // BIAS_GELU / BIAS_QGELU: C = act'(pre) (what the backward needs), aux_out = act(pre);
 // GELU_BWD / QGELU_BWD: C = acc * aux, aux = that saved act'(pre)  (same for both).
 enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_PATCH = 4,
@@ -644,19 +650,32 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
   };
   lane_offsets(std::integral_constant<int, PL>{}, std::integral_constant<int, BM>{}, poff, C::GP, ldp, i0, M);
   lane_offsets(std::integral_constant<int, QL>{}, std::integral_constant<int, BN>{}, qoff, C::GQ, ldq, j0, N);
-  auto issue = [&](int k) {
+  // part 1: the P pieces of stage k, part 2: the Q pieces, 3: both
+  auto issue = [&](int k, int part = 3) {
     char* buf = smem + (k % S) * C::STAGE;
     const int r = rb + k * BK;
     const char* pb = reinterpret_cast<const char*>(P) + (PL == LAY_RC ? (int64_t)r * 2 : (int64_t)r * ldp * 2);
     const char* qb = reinterpret_cast<const char*>(Q) + (QL == LAY_RC ? (int64_t)r * 2 : (int64_t)r * ldq * 2);
+    if (part & 1) {
 #pragma unroll
-    for (int u = 0; u < C::GP; ++u)
-      __builtin_amdgcn_global_load_lds((const void*)(pb + poff[u]), LDS_PTR(buf + (wave * C::GP + u) * 1024), 16, 0, 0);
+      for (int u = 0; u < C::GP; ++u)
+        __builtin_amdgcn_global_load_lds((const void*)(pb + poff[u]), LDS_PTR(buf + (wave * C::GP + u) * 1024), 16, 0,
+                                         0);
+    }
+    if (part & 2) {
 #pragma unroll
-    for (int u = 0; u < C::GQ; ++u)
-      __builtin_amdgcn_global_load_lds((const void*)(qb + qoff[u]), LDS_PTR(buf + C::PIMG + (wave * C::GQ + u) * 1024), 16,
-                                       0, 0);
+      for (int u = 0; u < C::GQ; ++u)
+        __builtin_amdgcn_global_load_lds((const void*)(qb + qoff[u]), LDS_PTR(buf + C::PIMG + (wave * C::GQ + u) * 1024),
+                                         16, 0, 0);
+    }
   };
+  // two k-substeps (BK = 64): the next stage's P pieces go out before the first substep's fragment
+  // reads, its Q pieces before the second's, instead of all of them behind the barrier (the waves of a
+  // SIMD reach the barrier together, so a burst of LDS-DMA issue there stalls both of their MFMA
+  // streams at once: +3-8 % main loop, tools/lab/mf32_lab.py, profiles/r04/gemm_load_split_lab.jsonl)
+  constexpr bool SPLIT_ISSUE = C::KS == 2 && VIT_SPLIT_ISSUE;
+  // one k-substep (BK = 32): the P pieces behind the barrier, the Q pieces behind the MFMAs
+  constexpr bool SPLIT_ISSUE1 = C::KS == 1 && VIT_SPLIT_ISSUE1;
   auto load_frags = [&](int k, int kk, bf16x8 (&pf)[C::AI], bf16x8 (&qf)[C::AJ]) {
     const char* cur = smem + (k % S) * C::STAGE;
 #pragma unroll
@@ -699,9 +718,13 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
       for (int kt = 0; kt < nk; ++kt) {
         wait_stages<C::G, S>(min(S - 2, nk - 1 - kt));
         if (!dbg_nobar) lds_barrier();
-        if (kt + S - 1 < nk && !dbg_noload) issue(kt + S - 1);
+        const bool more = kt + S - 1 < nk && !dbg_noload;
+        if (!SPLIT_ISSUE && more) issue(kt + S - 1, SPLIT_ISSUE1 ? 1 : 3);
         Unroll<C::KS>::run([&](auto kkI) {
           constexpr int kk = decltype(kkI)::value;
+          if constexpr (SPLIT_ISSUE) {
+            if (more) issue(kt + S - 1, kk + 1);
+          }
           // asm fragment reads (no compiler vmcnt(0) for the in-flight ring loads);
           // retired before the MFMAs, so they are also done before the next barrier (WAR)
           const uint32_t cur = lds_addr(smem + (kt % S) * C::STAGE);
@@ -739,6 +762,9 @@ __device__ __forceinline__ void gemm_tile(const bf16* __restrict__ P, int64_t ld
           lgkm_wait0();
           mma(pf, qf);
         });
+        if constexpr (SPLIT_ISSUE1) {
+          if (more) issue(kt + S - 1, 2);
+        }
       }
     } else {
       static_assert(C::KS == 1, "register double-buffering is built for BK = 32");
