@@ -95,11 +95,6 @@ _COL_BATCH = [os.environ.get("VIT_COL_BATCH", "1") != "0"]
 # VIT_WGRAD_PAIRS=0: each weight gradient as its own launch (with COL_BATCH) instead of fc2 + fc1 and
 # proj + qkv as one grouped launch each
 _WGRAD_PAIRS = [os.environ.get("VIT_WGRAD_PAIRS", "1") != "0"]
-# where the MLP weight-gradient pair goes onto the side stream (A/B): 0 = right after the fc2 input
-# gradient (its inputs are ready), 1 = after the LayerNorm-2 backward, 2 = after the proj input gradient,
-# 3 = after the attention backward (the side stream then waits for it: the attention backward and the
-# input gradients before it get the CUs the pair would hold)
-_MLP_PAIR_AT = [int(os.environ.get("VIT_WGRAD_MLP_AT", "0"))]
 
 
 def set_wgrad_overlap(enable: bool):
@@ -442,13 +437,6 @@ class _BlockFn(torch.autograd.Function):
         # gradient buffers are taken on the main stream (allocator ownership), filled on the side stream
         g = [None] * 13
         dpre = dxm = dxm_c = do = dqkv = None
-        mlp_pair = None  # the MLP weight-gradient pair while its launch is held back (_MLP_PAIR_AT)
-
-        def launch_mlp_pair(at):
-            nonlocal mlp_pair
-            if mlp_pair is not None and (at is None or _MLP_PAIR_AT[0] == at):
-                side.run(mlp_pair)
-                mlp_pair = None
         for i, p in ((1, n1w), (2, n1b), (3, qkvw), (4, qkvb), (5, projw), (6, projb), (7, n2w), (8, n2b),
                      (9, fc1w), (10, fc1b), (11, fc2w), (12, fc2b)):
             if ng[i]:
@@ -476,9 +464,7 @@ class _BlockFn(torch.autograd.Function):
         if need_mlp_in:
             dpre = ops.linear_dgrad(dxo_c, W2, out_dtype=T, epi=gelu_bwd, pre=dact, dbias=g[10], reduce_on=rb)
             if pair_mlp:
-                mlp_pair = lambda: ops.linear_wgrad_pair((dxo_c, act, g[11]), (dpre, h2, g[9]), rbw)  # noqa: E731
-                if _MLP_PAIR_AT[0] == 0 or not any(ng[0:9]):
-                    launch_mlp_pair(None)
+                side.run(lambda: ops.linear_wgrad_pair((dxo_c, act, g[11]), (dpre, h2, g[9]), rbw))
             elif ng[9]:
                 side.run(lambda: ops.linear_wgrad(dpre, h2, out=g[9], reduce_on=rbw))
         if any(ng[0:9]):
@@ -488,7 +474,6 @@ class _BlockFn(torch.autograd.Function):
             ops.layer_norm_bwd(xm, D, dh2, n2w.detach(), m2, r2, dxm, D, M, dres=dxo, ldres=D,
                                dx_copy=None if T == torch.float32 else dxm_c, ld_copy=D, dgamma=g[7], dbeta=g[8],
                                dsum=g[6], reduce_on=rb)
-            launch_mlp_pair(1)
             # attention
             # block 0 (the patch rows' block, last in the backward): its last weight gradients are the tail
             tail = bool(compact_np)
@@ -497,15 +482,12 @@ class _BlockFn(torch.autograd.Function):
                 side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5], tail=tail, reduce_on=rbw))
             if need_attn:
                 do = ops.linear_dgrad(dxm_c, Wproj, out_dtype=T)
-                launch_mlp_pair(2)
                 dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g[4], causal=causal,
                                     reduce_on=rb if _COL_BATCH[0] else None)
-                launch_mlp_pair(None)  # 3, or whatever is still held: ahead of the attention pair
                 if pair_attn:
                     side.run(lambda: ops.linear_wgrad_pair((dxm_c, o, g[5]), (dqkv, h1, g[3]), rbw, tail=tail))
                 elif ng[3]:
                     side.run(lambda: ops.linear_wgrad(dqkv, h1, out=g[3], tail=tail, reduce_on=rbw))
-            launch_mlp_pair(None)
             if need_h1:
                 dh1 = ops.linear_dgrad(dqkv, Wqkv, out_dtype=T)
                 dx = torch.empty(M, D, dtype=torch.float32, device=dev)
