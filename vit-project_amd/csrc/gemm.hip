@@ -1312,7 +1312,8 @@ static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool per
                         bool act_fwd = false) {
   static const int o_fwd = env_variant("VIT_GEMM_FWD"), o_dgrad = env_variant("VIT_GEMM_DGRAD"),
                    o_wgrad = env_variant("VIT_GEMM_WGRAD"), o_fwd_small = env_variant("VIT_GEMM_FWD_SMALL"),
-                   o_fwd_gelu = env_variant("VIT_GEMM_FWD_GELU");
+                   o_fwd_gelu = env_variant("VIT_GEMM_FWD_GELU"), o_dgrad_small = env_variant("VIT_GEMM_DGRAD_SMALL"),
+                   o_dgrad_gelu = env_variant("VIT_GEMM_DGRAD_GELU");
   const bool wgrad = split > 1 || (pl == LAY_CR && ql == LAY_CR), fwd = pl == LAY_RC && ql == LAY_RC;
   const int o = wgrad ? o_wgrad : fwd ? o_fwd : o_dgrad;
   int v;
@@ -1323,6 +1324,8 @@ static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool per
   else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : (o_fwd_small >= 0 ? o_fwd_small : 5);  // forward
   // (the N, R < 1536 forwards -- proj, patch embedding -- moved from V2 to V5 in round 3: +0.35 % step,
   // same-box pairs, bit-identical loss trajectory; VIT_GEMM_FWD_SMALL=2 restores V2)
+  else if (act_bwd && o_dgrad_gelu >= 0) v = o_dgrad_gelu;                // per-shape A/B overrides of the
+  else if (!act_bwd && N <= 1024 && R <= 1024 && o_dgrad_small >= 0) v = o_dgrad_small;  // dgrad rule below
   else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;                // dgrad (GELU' epilogue: V1, 2 WG/CU)
   (void)M;
   if ((v == 2 || v == 5 || v == 10) && R % 64) v = 1;                       // BK = 64 configurations need 64-row chunks
