@@ -55,6 +55,16 @@ for _ in range(reps):
             ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dqkv=dq)
     elif which == "dgrad_fc1":
         ops.linear_dgrad(dy, w, out_dtype=bf)
+    elif which in ("dgrad_fc2_gelu", "dgrad_fc2_plain"):  # the step's fc2 input gradient, with / without GELU'
+        if _ == 0:
+            dy2 = torch.randn(M, D, device=dev).to(bf)
+            w2 = (torch.randn(D, F, device=dev) * 0.05).to(bf)
+            pre = torch.randn(M, F, device=dev).to(bf)
+            dpre = torch.empty(M, F, device=dev, dtype=bf)
+        if which == "dgrad_fc2_gelu":
+            ops.linear_dgrad(dy2, w2, out_dtype=bf, epi=L.EPI_GELU_BWD, pre=pre, out=dpre)
+        else:
+            ops.linear_dgrad(dy2, w2, out_dtype=bf, out=dpre)
 torch.cuda.synchronize()
 print("done", which)
 if which in ("sdpa_bwd", "sdpa_fwd"):
