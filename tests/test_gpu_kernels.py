@@ -662,6 +662,44 @@ def test_sdpa_bwd_banded_matches_whole_head(N, causal):
     _close(b1, b0, 1e-5, "qkv bias grad (banded vs fused)")
 
 
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+def test_gemm_ms_matches_default(cfg):
+    """The opt-in multi-tile deferred-store GEMM (csrc/gemm_ms.hip, round 4) against the default
+    one-tile path on the same inputs: forward store, forward GELU pair, input gradient (W [K][N]);
+    bit-identical (same k-order per output).  Ragged M (not a multiple of the 192 / 256-row tiles), and
+    a grid smaller than the tile count, so workgroups run several tiles and defer stores across them."""
+    lib = L.lib()
+    lib.vit_gemm_ms_config(0, -1, -1)
+    bf = torch.bfloat16
+    st = torch.cuda.current_stream().cuda_stream
+    M = 1000
+    for K, N, epi, wl in [(768, 2304, 0, 0), (768, 768, 0, 0), (768, 3072, 1, 0), (3072, 768, 0, 1)]:
+        x = _rnd(M, K, seed=K + N, dtype=bf).to(DEV)
+        w = _rnd(*((K, N) if wl else (N, K)), seed=7, scale=0.05, dtype=bf).to(DEV)
+        b = None if wl else _rnd(N, seed=9).to(DEV)
+        y0, y1 = torch.empty(M, N, device=DEV, dtype=bf), torch.empty(M, N, device=DEV, dtype=bf)
+        if wl:
+            ops.linear_dgrad(x, w, out_dtype=bf, out=y0)
+        elif epi:
+            ops.linear_fwd(x, w, b, epi=L.EPI_BIAS_GELU, out=y0, act_out=y1)
+        else:
+            ops.linear_fwd(x, w, b, out=y0)
+        for grid in (0, 7):
+            z0, z1 = torch.zeros_like(y0), torch.zeros_like(y1)
+            rc = lib.vit_gemm_ms(epi, wl, cfg, M, N, K, x.data_ptr(), K, w.data_ptr(), N if wl else K,
+                                 None if b is None else b.data_ptr(), z0.data_ptr(), N,
+                                 z1.data_ptr() if epi else None, grid, st)
+            assert rc == 0, rc
+            torch.cuda.synchronize()
+            assert torch.equal(z0, y0), (K, N, epi, wl, grid, (z0.float() - y0.float()).abs().max().item())
+            if epi:
+                assert torch.equal(z1, y1), (K, N, grid)
+    # outside the contract (N % 256): refused, nothing launched
+    z = torch.empty(M, 200, device=DEV, dtype=bf)
+    assert lib.vit_gemm_ms(0, 0, cfg, M, 200, 768, x.data_ptr(), 768, x.data_ptr(), 768, None, z.data_ptr(),
+                           200, None, 0, st) != 0
+
+
 @pytest.mark.parametrize("N", [77, 16, 197, 224])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 def test_sdpa_causal_fwd_bwd(N, dtype):
