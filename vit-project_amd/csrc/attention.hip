@@ -813,7 +813,7 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
 #pragma unroll
   for (int dt = 0; dt < 4; ++dt) { dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[dt] = dv[dt]; }
   char* dsw = dST + key * 32 + g * 8;  // this lane's dS^T slot (queries 4g..4g+3 of a column tile)
-#pragma unroll 1
+#pragma unroll
   for (int qp = 0; qp < NT2; ++qp) {
     f32x4 p[2], ds[2];
 #pragma unroll
