@@ -92,9 +92,16 @@ _FUSED_RESID_F32 = [os.environ.get("VIT_FUSED_RESID_F32", "0") == "1"]
 # VIT_COL_BATCH=0: every bias / LayerNorm-affine reduction of a block's backward as its own launch(es)
 # (the round-2 schedule: ~9 launches per block) instead of one vit_colreduce_batch launch per block
 _COL_BATCH = [os.environ.get("VIT_COL_BATCH", "1") != "0"]
-# VIT_WGRAD_PAIRS=0: each weight gradient as its own launch (with COL_BATCH) instead of fc2 + fc1 and
-# proj + qkv as one grouped launch each
-_WGRAD_PAIRS = [os.environ.get("VIT_WGRAD_PAIRS", "1") != "0"]
+# VIT_WGRAD_PAIRS: 1 (default) = fc2 + fc1 and proj + qkv weight gradients as one grouped launch each;
+# 0 = each as its own launch (with COL_BATCH; fc2's and proj's then start before their block's input-
+# gradient kernels, as soon as their operands exist); 2 = only the MLP pair grouped; 3 = only the
+# attention pair grouped
+_WGRAD_PAIRS = [os.environ.get("VIT_WGRAD_PAIRS", "1")]
+
+
+def _pair_on(which: str) -> bool:
+    v = _WGRAD_PAIRS[0]
+    return v == "1" or (v == "2" and which == "mlp") or (v == "3" and which == "attn")
 
 
 def set_wgrad_overlap(enable: bool):
@@ -457,7 +464,7 @@ class _BlockFn(torch.autograd.Function):
                 ops.colsum(dxo_c, out=g[12])
         # weight gradients in pairs over the same token rows (fc2 + fc1, proj + qkv): one grouped
         # launch each, half the split-K slabs of two launches (VIT_WGRAD_PAIRS=0: one launch each)
-        pair_mlp = rbw is not None and _WGRAD_PAIRS[0] and ng[11] and ng[9] and need_mlp_in
+        pair_mlp = rbw is not None and _pair_on("mlp") and ng[11] and ng[9] and need_mlp_in
         if ng[11] and not pair_mlp:
             side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g[11], reduce_on=rbw))
         dx = None
@@ -477,7 +484,7 @@ class _BlockFn(torch.autograd.Function):
             # attention
             # block 0 (the patch rows' block, last in the backward): its last weight gradients are the tail
             tail = bool(compact_np)
-            pair_attn = rbw is not None and _WGRAD_PAIRS[0] and ng[5] and ng[3] and need_attn
+            pair_attn = rbw is not None and _pair_on("attn") and ng[5] and ng[3] and need_attn
             if ng[5] and not pair_attn:
                 side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5], tail=tail, reduce_on=rbw))
             if need_attn:
