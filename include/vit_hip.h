@@ -146,6 +146,17 @@ int vit_patch_embed_fwd(int dtype, int B, int np, int D, int K, const void* U, c
                         const float* bias, const float* pos, float* x, void* stream);
 /* Conv2d 16/16 unfold: img f32 [B,C,H,W] -> U [B*np, C*ps*ps] (column = c*ps*ps+ky*ps+kx). */
 int vit_patch_unfold(int dtype, int B, int C, int Hi, int Wi, int ps, const float* img, void* U, void* stream);
+/* ABI 7: the same with U rows ldu >= C*ps*ps elements apart, columns [C*ps*ps, ldu) zero-filled, and the
+ * patch embedding over such rows (K = the padded reduction length, W [D][ldw] zero past the real
+ * columns): CLIP ViT-L/14's 3*14*14 = 588 columns padded to 608 run on the MFMA GEMM instead of the
+ * scalar-FMA kernel (NEWP:274's visual conv1).  vit_copy_rows_padded builds such a W: dst[r][c] =
+ * src[r][c] for c < cols, 0 up to ld_dst. */
+int vit_patch_unfold_ld(int dtype, int B, int C, int Hi, int Wi, int ps, int ldu, const float* img, void* U,
+                        void* stream);
+int vit_patch_embed_fwd_ld(int dtype, int B, int np, int D, int K, const void* U, int64_t ldu, const void* W,
+                           int64_t ldw, const float* bias, const float* pos, float* x, void* stream);
+int vit_copy_rows_padded(int dtype, int rows, int cols, const void* src, int64_t ld_src, void* dst, int64_t ld_dst,
+                         void* stream);
 /* cat(cls_token) + pos_embed[0] into row 0 of every image (timm _pos_embed). */
 int vit_cls_pos_fill(int B, int S, int D, float* x, const float* cls, const float* pos, void* stream);
 /* d pos_embed [S,D] = sum_b dx[b]; d cls_token = d pos_embed[0]. */

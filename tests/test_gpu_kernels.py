@@ -451,6 +451,32 @@ def test_patch_embed_fwd_and_unfold():
         _close(x, ref, rel if dt == torch.float32 else 2e-3, f"patch {dt}")
 
 
+def test_patch_embed_padded_reduction_on_mfma_path():
+    """CLIP ViT-L/14's patch embedding (ps = 14: 588 columns) with U and the weight zero-padded to
+    608 columns (vit_patch_unfold_ld / vit_copy_rows_padded, ABI 7), so the GEMM takes the MFMA
+    path: the padded U rows hold the unfolded patch plus exact zeros, and the output matches a
+    torch fp32 conv (f32: 1e-5 of scale; bf16 operands: 2e-3).  M = 2 x 256 patches x 2 images."""
+    B, D, ps = 2, 1024, 14
+    img = _rnd(B, 3, 224, 224, seed=30)
+    w = _rnd(D, 3, ps, ps, seed=31, scale=0.02)
+    pos = _rnd(1, 257, D, seed=33)
+    cls = _rnd(1, 1, D, seed=34)
+    np_ = 256
+    K, Kp = 3 * ps * ps, 608
+    for dt, rel in ((torch.float32, 1e-5), (torch.bfloat16, 2e-3)):
+        U = ops.patch_unfold(img.to(DEV), ps, dt, ld=Kp)
+        assert U.shape == (B * np_, Kp)
+        ref_u = img.unfold(2, ps, ps).unfold(3, ps, ps).permute(0, 2, 3, 1, 4, 5).reshape(B * np_, -1)
+        assert torch.equal(U[:, :K].cpu(), ref_u.to(dt))
+        assert not U[:, K:].float().abs().any().item()
+        wp = ops.pad_cols(w.reshape(D, -1).to(dt).to(DEV), Kp)
+        assert torch.equal(wp[:, :K].cpu(), w.reshape(D, -1).to(dt)) and not wp[:, K:].float().abs().any().item()
+        x = ops.patch_embed_fwd(U, wp, None, pos.reshape(-1, D).to(DEV), cls.reshape(-1).to(DEV), B, np_)
+        y = torch.nn.functional.conv2d(img, w.to(dt).float(), None, stride=ps).flatten(2).transpose(1, 2)
+        ref = torch.cat([cls.expand(B, -1, -1), y], 1) + pos
+        _close(x, ref, rel, f"padded patch {dt}")
+
+
 # ---------------------------------------------------------------------------- LayerNorm
 
 @pytest.mark.parametrize("D", [768, 1024, 64, 200])

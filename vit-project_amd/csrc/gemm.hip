@@ -1937,11 +1937,17 @@ int vit_colsum(int dtype, int M, int N, const void* X, int64_t ld, float* out, f
 // Patch embedding forward (timm PatchEmbed Conv2d 16/16 + _pos_embed):
 //   x[b*(np+1) + 1 + p][n] = U[b*np + p] . Wpe[n] + bpe[n] + pos[1+p][n]   (f32 out)
 // U = unfolded patches [B*np, K] (vit_patch_unfold).  CLS rows: vit_cls_pos_fill.
-int vit_patch_embed_fwd(int dtype, int B, int np, int D, int K, const void* U, const void* W,
-                        const float* bias, const float* pos, float* x, void* stream) {
+int vit_patch_embed_fwd_ld(int dtype, int B, int np, int D, int K, const void* U, int64_t ldu, const void* W,
+                           int64_t ldw, const float* bias, const float* pos, float* x, void* stream) {
+  if (ldu < K || ldw < K) return (int)hipErrorInvalidValue;
   Epi e = make_epi();
   e.C = x; e.ldc = D; e.bias = bias; e.pos = pos; e.n_patch = np;
-  return gemm_any(EPI_PATCH, dtype, VIT_F32, LAY_RC, LAY_RC, B * np, D, K, U, K, W, K, 1, e, (hipStream_t)stream);
+  return gemm_any(EPI_PATCH, dtype, VIT_F32, LAY_RC, LAY_RC, B * np, D, K, U, ldu, W, ldw, 1, e, (hipStream_t)stream);
+}
+
+int vit_patch_embed_fwd(int dtype, int B, int np, int D, int K, const void* U, const void* W,
+                        const float* bias, const float* pos, float* x, void* stream) {
+  return vit_patch_embed_fwd_ld(dtype, B, np, D, K, U, K, W, K, bias, pos, x, stream);
 }
 
 }  // extern "C"

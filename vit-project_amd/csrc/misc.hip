@@ -11,7 +11,7 @@
 // ---------------------------------------------------------------------------
 template <typename T>
 __global__ void patch_unfold_kernel(const float* __restrict__ img, T* __restrict__ U, int B, int C, int Hi, int Wi,
-                                    int ps) {
+                                    int ps, int ldu) {
   const int gh = Hi / ps, gw = Wi / ps;
   int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t total = (int64_t)B * C * gh * ps * gw;
@@ -22,9 +22,12 @@ __global__ void patch_unfold_kernel(const float* __restrict__ img, T* __restrict
   int c = t % C; int b = (int)(t / C);
   const float* src = img + (((int64_t)b * C + c) * Hi + py * ps + ky) * Wi + px * ps;
   const int K = C * ps * ps;
-  T* dst = U + ((int64_t)b * gh * gw + py * gw + px) * K + c * ps * ps + ky * ps;
+  T* urow = U + ((int64_t)b * gh * gw + py * gw + px) * ldu;
+  T* dst = urow + c * ps * ps + ky * ps;
+  if (c == 0 && ky == 0)  // the row's padding columns [K, ldu) (a GEMM reduction padded to its tile depth)
+    for (int k = K; k < ldu; ++k) urow[k] = (T)0.f;
   if constexpr (std::is_same<T, bf16>::value) {
-    if (ps == 16 && (K % 8) == 0 && ((uintptr_t)U & 15) == 0 && (Wi % 4) == 0 && ((uintptr_t)img & 15) == 0) {
+    if (ps == 16 && (ldu % 8) == 0 && ((uintptr_t)U & 15) == 0 && (Wi % 4) == 0 && ((uintptr_t)img & 15) == 0) {
       // one 64-B row segment in, two 16-B stores out (consecutive threads: consecutive patches)
       f32x4 v[4];
 #pragma unroll
@@ -46,6 +49,15 @@ __global__ void patch_unfold_kernel(const float* __restrict__ img, T* __restrict
   } else {
     for (int kx = 0; kx < ps; ++kx) dst[kx] = (T)src[kx];
   }
+}
+
+template <typename T>
+__global__ void copy_rows_pad_kernel(const T* __restrict__ src, int64_t lds, T* __restrict__ dst, int64_t ldd,
+                                     int cols, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int64_t r = i / ldd, c = i - r * ldd;
+  dst[i] = c < cols ? src[r * lds + c] : (T)0.f;
 }
 
 // x[b*S + 0][j] = cls[j] + pos[0][j]
@@ -209,13 +221,39 @@ __global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restri
 
 extern "C" {
 
-int vit_patch_unfold(int dtype, int B, int C, int Hi, int Wi, int ps, const float* img, void* U, void* stream) {
+int vit_patch_unfold_ld(int dtype, int B, int C, int Hi, int Wi, int ps, int ldu, const float* img, void* U,
+                        void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (Hi % ps || Wi % ps) return (int)hipErrorInvalidValue;
+  if (Hi % ps || Wi % ps || ldu < C * ps * ps) return (int)hipErrorInvalidValue;
   int64_t total = (int64_t)B * C * (Hi / ps) * ps * (Wi / ps);
   dim3 grid((unsigned)((total + 255) / 256));
-  if (dtype == VIT_BF16) hipLaunchKernelGGL(patch_unfold_kernel<bf16>, grid, dim3(256), 0, s, img, (bf16*)U, B, C, Hi, Wi, ps);
-  else hipLaunchKernelGGL(patch_unfold_kernel<float>, grid, dim3(256), 0, s, img, (float*)U, B, C, Hi, Wi, ps);
+  if (dtype == VIT_BF16)
+    hipLaunchKernelGGL(patch_unfold_kernel<bf16>, grid, dim3(256), 0, s, img, (bf16*)U, B, C, Hi, Wi, ps, ldu);
+  else
+    hipLaunchKernelGGL(patch_unfold_kernel<float>, grid, dim3(256), 0, s, img, (float*)U, B, C, Hi, Wi, ps, ldu);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+int vit_patch_unfold(int dtype, int B, int C, int Hi, int Wi, int ps, const float* img, void* U, void* stream) {
+  return vit_patch_unfold_ld(dtype, B, C, Hi, Wi, ps, C * ps * ps, img, U, stream);
+}
+
+// dst[r][c] = src[r][c] for c < cols, 0 for cols <= c < ld_dst (a weight matrix padded along its
+// reduction dimension to the GEMM tile depth)
+int vit_copy_rows_padded(int dtype, int rows, int cols, const void* src, int64_t ld_src, void* dst, int64_t ld_dst,
+                         void* stream) {
+  if (rows < 0 || cols < 0 || ld_src < cols || ld_dst < cols) return (int)hipErrorInvalidValue;
+  const int64_t total = (int64_t)rows * ld_dst;
+  if (total == 0) return 0;
+  dim3 grid((unsigned)((total + 255) / 256));
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == VIT_BF16)
+    hipLaunchKernelGGL(copy_rows_pad_kernel<bf16>, grid, dim3(256), 0, s, (const bf16*)src, ld_src, (bf16*)dst, ld_dst,
+                       cols, total);
+  else
+    hipLaunchKernelGGL(copy_rows_pad_kernel<float>, grid, dim3(256), 0, s, (const float*)src, ld_src, (float*)dst,
+                       ld_dst, cols, total);
   VIT_CHECK_LAUNCH();
   return 0;
 }
@@ -293,6 +331,6 @@ int vit_zero(void* p, int64_t bytes, void* stream) {
   return (int)hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);
 }
 
-int vit_abi_version(void) { return 6; }
+int vit_abi_version(void) { return 7; }
 
 }  // extern "C"

@@ -46,6 +46,7 @@ SIGNATURES = {
                                    i64, vp],
     "vit_colsum": [i32, i32, i32, vp, i64, vp, vp, i64, i32, vp],
     "vit_patch_embed_fwd": [i32, i32, i32, i32, i32, vp, vp, vp, vp, vp, vp],
+    "vit_patch_embed_fwd_ld": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp],
     "vit_layer_norm_fwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, f32, vp],
     "vit_add_layer_norm_fwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, i64, vp, vp, vp, vp, f32, vp],
     "vit_layer_norm_bwd": [i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, vp, vp, i64, vp, i64, vp, i64, i32,
@@ -59,6 +60,8 @@ SIGNATURES = {
     "vit_sdpa_bwd": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, f32, i32, vp, vp, i64, vp],
     "vit_sdpa_bwd_partial_floats": [i32, i32, i32],
     "vit_patch_unfold": [i32, i32, i32, i32, i32, i32, vp, vp, vp],
+    "vit_patch_unfold_ld": [i32, i32, i32, i32, i32, i32, i32, vp, vp, vp],
+    "vit_copy_rows_padded": [i32, i32, i32, vp, i64, vp, i64, vp],
     "vit_cls_pos_fill": [i32, i32, i32, vp, vp, vp, vp],
     "vit_pos_grad": [i32, i32, i32, vp, vp, vp, vp],
     "vit_cross_entropy_fwd": [i32, i32, vp, i64, vp, vp, vp, vp, vp],

@@ -36,6 +36,7 @@ is bit-identical to recomputing it.
 from __future__ import annotations
 
 import math
+import os
 from collections import OrderedDict
 
 import torch
@@ -47,6 +48,22 @@ from .dora import DoRALayer
 from .model import _FUSED_RESID, _FUSED_RESID_F32, _BlockFn, _Shadowed, _gout, _wt
 
 SOT, EOT = 49406, 49407
+
+
+# VIT_CLIP_PATCH_PAD=0: the unpadded 588-column patch embedding (scalar-FMA GEMM) -- A/B only
+_PATCH_PAD = [os.environ.get("VIT_CLIP_PATCH_PAD", "1") != "0"]
+
+
+def _padded_weight(mod, w2, Kp):
+    """``w2`` [D, K] zero-padded to [D, Kp], cached on ``mod`` until the weight (or its bf16 shadow)
+    changes: the conv1 weight is frozen on the CLIP-HBA path, so this runs once."""
+    p = mod.weight
+    key = (w2.data_ptr(), w2.dtype, p._version, getattr(p, "_vit_shadow_version", None), Kp)
+    hit = getattr(mod, "_vit_wpad", None)
+    if hit is None or hit[0] != key:
+        hit = (key, ops.pad_cols(w2, Kp))
+        mod._vit_wpad = hit
+    return hit[1]
 
 
 # ----------------------------------------------------------------------------
@@ -318,12 +335,18 @@ class CLIP(nn.Module):
         B = image.shape[0]
         ps = v.patch_size
         W = v.conv1.out_channels
-        U = ops.patch_unfold(image.to(torch.float32).contiguous(), ps, T)
+        # ViT-L/14's 3*14*14 = 588 patch columns are padded to a multiple of the GEMM's 32-deep k-step
+        # (zeros in U and in the weight), so the patch embedding runs on the MFMA path
+        K = v.conv1.in_channels * ps * ps
+        Kp = -(-K // 32) * 32 if _PATCH_PAD[0] else K
+        U = ops.patch_unfold(image.to(torch.float32).contiguous(), ps, T, ld=Kp)
         npatch = U.shape[0] // B
         pos = v.positional_embedding.detach()
         if not pos_embedding:
             pos = ops.zero_(torch.empty_like(pos))
         w2 = _wt(v.conv1.weight, T).reshape(W, -1)
+        if Kp != K:
+            w2 = _padded_weight(v.conv1, w2, Kp)
         x = ops.patch_embed_fwd(U, w2, None, pos.contiguous(), v.class_embedding.detach().contiguous(), B, npatch)
         x2, _, _ = ops.layer_norm_fwd(x.reshape(B * (npatch + 1), W), v.ln_pre.weight.detach(),
                                       v.ln_pre.bias.detach(), 1e-5, torch.float32, need_stats=False)

@@ -429,19 +429,35 @@ def sdpa_bwd(qkv2d, o, do, lse, B, H, N, dqkv=None, scale=None, dbias=None, caus
 # patch embed, CE, casts
 # ----------------------------------------------------------------------------
 
-def patch_unfold(img, ps, dtype):
+def patch_unfold(img, ps, dtype, ld=None):
+    """U [B*np, C*ps*ps]; with ``ld`` > C*ps*ps the rows are ``ld`` wide and the extra columns zero (a
+    reduction padded to the GEMM tile depth, for padded weights from :func:`pad_cols`)."""
     B, C, Hi, Wi = img.shape
     assert img.dtype == torch.float32 and img.is_contiguous()
     npatch = (Hi // ps) * (Wi // ps)
-    U = torch.empty(B * npatch, C * ps * ps, dtype=dtype, device=img.device)
-    call("vit_patch_unfold", L.dt(U), B, C, Hi, Wi, ps, ptr(img), ptr(U), _s(img))
+    K = C * ps * ps
+    U = torch.empty(B * npatch, max(K, ld or K), dtype=dtype, device=img.device)
+    call("vit_patch_unfold_ld", L.dt(U), B, C, Hi, Wi, ps, U.shape[1], ptr(img), ptr(U), _s(img))
     return U
 
 
+def pad_cols(w2d, ld):
+    """[rows, cols] -> [rows, ld] with columns [cols, ld) zero (vit_copy_rows_padded)."""
+    rows, cols = w2d.shape
+    assert w2d.stride(1) == 1 and ld >= cols
+    out = torch.empty(rows, ld, dtype=w2d.dtype, device=w2d.device)
+    call("vit_copy_rows_padded", L.dt(w2d), rows, cols, ptr(w2d), w2d.stride(0), ptr(out), ld, _s(w2d))
+    return out
+
+
 def patch_embed_fwd(U, w2d, bias, pos, cls, B, npatch):
+    """x[b, 1 + p] = U[b*np + p] . w2d + bias + pos[1 + p]; U and w2d may both carry zero padding
+    columns (same width)."""
     D, K = w2d.shape
+    assert U.shape[1] == K and U.stride(1) == 1 and w2d.stride(1) == 1
     x = torch.empty(B, npatch + 1, D, dtype=torch.float32, device=U.device)
-    call("vit_patch_embed_fwd", L.dt(U), B, npatch, D, K, ptr(U), ptr(w2d), ptr(bias), ptr(pos), ptr(x), _s(U))
+    call("vit_patch_embed_fwd_ld", L.dt(U), B, npatch, D, K, ptr(U), U.stride(0), ptr(w2d), w2d.stride(0),
+         ptr(bias), ptr(pos), ptr(x), _s(U))
     call("vit_cls_pos_fill", B, npatch + 1, D, ptr(x), ptr(cls), ptr(pos), _s(U))
     return x
 
