@@ -244,6 +244,14 @@ int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, 
 int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, const float* B, const float* gW,
                         const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
                         float* sdDnT_ws, const float* noise, void* stream);
+/* ABI 7: the same with a split-K slab workspace (slab_floats >= 2 * 256 * 1024 lets every factor GEMM split;
+ * nullptr / 0 = unsplit), and the split-K GEMM it uses: C [M][N] contiguous f32 = sum_r P(i,r) Q(j,r) in
+ * r-chunks of >= 128 summed in chunk order (deterministic). */
+int vit_dora_weight_bwd_ws(int in, int out, int r, const float* m, const float* A, const float* B, const float* gW,
+                           const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
+                           float* sdDnT_ws, float* slabs, int64_t slab_floats, const float* noise, void* stream);
+int vit_gemm_splitk(int p_layout, int q_layout, int M, int N, int R, const float* P, int64_t ldp, const float* Q,
+                    int64_t ldq, float* C, float* slabs, int64_t slab_floats, void* stream);
 /* torch.optim.AdamW step (NEWP:1181, NEWP:1001): tensors {float* p; const float* g; float* exp_avg;
  * float* exp_avg_sq; bf16* shadow (or null); int64 n; const float* coef}[] where coef points at
  * the tensor's {step_size, bc2_sqrt, decay, 0} in device memory: step_size = lr / (1 - beta1^step),

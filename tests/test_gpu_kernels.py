@@ -477,6 +477,35 @@ def test_patch_embed_padded_reduction_on_mfma_path():
         _close(x, ref, rel, f"padded patch {dt}")
 
 
+@pytest.mark.parametrize("M,N,R", [(64, 66, 768), (32, 1024, 4096), (1024, 32, 1024), (64, 768, 1024)])
+def test_gemm_splitk_matches_reference(M, N, R):
+    """vit_gemm_splitk (round 4: DoRA factor gradients, CLIP-HBA head GEMMs): every layout pair against a
+    float64 product at 1e-5 of scale, two runs bit-identical (slab sum in a fixed order), and the
+    unsplit fallback (no slab room) within the same bound."""
+    lib = L.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    g = torch.Generator().manual_seed(M + N + R)
+    slabs = torch.empty(2 * 256 * 1024, device=DEV)
+    for pl in (L.LAY_RC, L.LAY_CR):
+        for ql in (L.LAY_RC, L.LAY_CR):
+            Pm = torch.randn(M, R, generator=g)  # P(i, r)
+            Qm = torch.randn(N, R, generator=g)
+            Pd = (Pm if pl == L.LAY_RC else Pm.t()).contiguous().to(DEV)
+            Qd = (Qm if ql == L.LAY_RC else Qm.t()).contiguous().to(DEV)
+            ref = (Pm.double() @ Qm.double().t()).float()
+            outs = []
+            for room in (slabs.numel(), slabs.numel(), 0):
+                c = torch.empty(M, N, device=DEV)
+                rc = lib.vit_gemm_splitk(pl, ql, M, N, R, Pd.data_ptr(), Pd.stride(0), Qd.data_ptr(), Qd.stride(0),
+                                         c.data_ptr(), slabs.data_ptr() if room else None, room, st)
+                assert rc == 0, rc
+                torch.cuda.synchronize()
+                outs.append(c.cpu())
+            _close(outs[0], ref, 1e-5, f"splitk {pl}{ql}")
+            _close(outs[2], ref, 1e-5, f"unsplit {pl}{ql}")
+            assert torch.equal(outs[0], outs[1])
+
+
 # ---------------------------------------------------------------------------- LayerNorm
 
 @pytest.mark.parametrize("D", [768, 1024, 64, 200])

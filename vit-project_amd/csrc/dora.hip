@@ -19,6 +19,8 @@ extern "C" int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, in
                         const void* P, int64_t ldp, const void* Q, int64_t ldq, void* C, int64_t ldc,
                         const float* bias, const void* aux, int64_t ld_aux, void* aux_out, int allow_fast,
                         void* stream);
+extern "C" int vit_gemm_splitk(int p_layout, int q_layout, int M, int N, int R, const float* P, int64_t ldp,
+                               const float* Q, int64_t ldq, float* C, float* slabs, int64_t slab_floats, void* stream);
 
 constexpr int DT = 64;
 
@@ -150,20 +152,27 @@ int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, 
 
 // Backward of vit_dora_weight_fwd given gW = dL/dW [out, in]; DnT/nu from the forward.
 // sdDnT_ws >= out*in floats.  Outputs dm [out], dA [r, out], dB [in, r] (f32, overwritten).
-int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, const float* Bm, const float* gW,
-                        const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
-                        float* sdDnT_ws, const float* noise, void* stream) {
+// ABI 7: slabs / slab_floats (>= 2 * max(in, out) * r floats to split) let the two factor GEMMs split their
+// 1024-4096-long reductions (vit_gemm_splitk); nullptr / 0 = the unsplit launches of vit_dora_weight_bwd.
+int vit_dora_weight_bwd_ws(int in, int out, int r, const float* m, const float* A, const float* Bm, const float* gW,
+                           const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
+                           float* sdDnT_ws, float* slabs, int64_t slab_floats, const float* noise, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(dora_bwd_row_kernel, dim3((out + 3) / 4), dim3(256), 0, s, in, out, gW, DnT, m, nu, scaling,
                      noise, dm, sdDnT_ws);
   VIT_CHECK_LAUNCH();
   // dB[i][k] = sum_o sdDnT[o][i] * A[k][o]:  P(i,o) = sdDnT[o*in + i] (CR), Q(k,o) = A[k*out + o] (RC)
-  int rc = vit_gemm(VIT_F32, VIT_F32, 1, 0, 0, in, r, out, sdDnT_ws, in, A, out, dB, r, nullptr, nullptr, 0, nullptr, 0,
-                    stream);
+  int rc = vit_gemm_splitk(1, 0, in, r, out, sdDnT_ws, in, A, out, dB, slabs, slab_floats, stream);
   if (rc) return rc;
   // dA[k][o] = sum_i B[i][k] * sdDnT[o][i]:  P(k,i) = B[i*r + k] (CR), Q(o,i) = sdDnT[o*in + i] (RC)
-  return vit_gemm(VIT_F32, VIT_F32, 1, 0, 0, r, out, in, Bm, r, sdDnT_ws, in, dA, out, nullptr, nullptr, 0, nullptr, 0,
-                  stream);
+  return vit_gemm_splitk(1, 0, r, out, in, Bm, r, sdDnT_ws, in, dA, slabs, slab_floats, stream);
+}
+
+int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, const float* Bm, const float* gW,
+                        const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
+                        float* sdDnT_ws, const float* noise, void* stream) {
+  return vit_dora_weight_bwd_ws(in, out, r, m, A, Bm, gW, DnT, scaling, nu, dm, dA, dB, sdDnT_ws, nullptr, 0, noise,
+                                stream);
 }
 
 // Fused AdamW over a table of AdamTensor {p, g, m, v, shadow, n, coef -> {step_size, bc2_sqrt, decay, 0}};

@@ -1673,6 +1673,36 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
                   (hipStream_t)stream, allow_fast != 0);
 }
 
+// f32 C[M][N] (contiguous) = sum_r P(i,r) Q(j,r) split along r on the generic kernel for small outputs over
+// long reductions (DoRA's factor gradients: [in x r] / [r x out] over out / in = 1024..4096 products, 24-32
+// workgroups unsplit): chunks of >= 128 products into slabs[z][M][N], then one slab sum in slab order
+// (deterministic).  Without room for two slabs it is the unsplit launch.
+int vit_gemm_splitk(int p_layout, int q_layout, int M, int N, int R, const float* P, int64_t ldp, const float* Q,
+                    int64_t ldq, float* C, float* slabs, int64_t slab_floats, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  if (M <= 0 || N <= 0) return 0;
+  const int64_t mn = (int64_t)M * N;
+  const int tiles = ((N + 31) / 32) * ((M + 31) / 32);
+  int split = 256 / (tiles > 0 ? tiles : 1);
+  if (split > R / 128) split = R / 128;
+  if (slabs == nullptr || (mn % 4) || ((uintptr_t)slabs & 15) || ((uintptr_t)C & 15)) split = 1;
+  while (split > 1 && (int64_t)split * mn > slab_floats) --split;
+  Epi e = make_epi();
+  if (split < 2) {
+    e.C = C; e.ldc = N;
+    return gemm_any(EPI_STORE, VIT_F32, VIT_F32, p_layout, q_layout, M, N, R, P, ldp, Q, ldq, 1, e, s, false);
+  }
+  const int r_chunk = r_chunk_for(R, split, gen::TK);
+  const int nz = (R + r_chunk - 1) / r_chunk;
+  e.C = slabs; e.ldc = N; e.slab = mn;
+  const int rc = gemm_any(EPI_STORE, VIT_F32, VIT_F32, p_layout, q_layout, M, N, R, P, ldp, Q, ldq, split, e, s, false);
+  if (rc) return rc;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((mn / 4 + 255) / 256 + 1)), dim3(256), 0, s,
+                     (const float*)slabs, nz, mn, C);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
 // The multi-tile deferred-store kernel (gemm_ms.hip) for the bf16 forwards (plain / GELU pair) and the
 // plain bf16 input gradients: VIT_GEMM_MS = bit mask (1 = forwards, 2 = input gradients; 0 = off, A/B),
 // VIT_GEMM_MS_CFG = its configuration (vit_gemm_ms cfg: row tile and store deferral), VIT_GEMM_MS_T =

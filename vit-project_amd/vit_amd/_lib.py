@@ -74,6 +74,8 @@ SIGNATURES = {
     "vit_zero": [vp, i64, vp],
     "vit_dora_weight_fwd": [i32, i32, i32, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp],
     "vit_dora_weight_bwd": [i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, vp],
+    "vit_dora_weight_bwd_ws": [i32, i32, i32, vp, vp, vp, vp, vp, f32, vp, vp, vp, vp, vp, vp, i64, vp, vp],
+    "vit_gemm_splitk": [i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, i64, vp],
     "vit_adamw_step": [vp, vp, i32, f32, f32, f32, vp],
     "vit_adamw_tensor_bytes": [],
     "vit_token_embed": [i32, i32, i32, i32, vp, vp, vp, vp, vp],

@@ -13,6 +13,7 @@ reads ``.weight``: quirk Q5, but part of the class's surface).
 from __future__ import annotations
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -21,6 +22,9 @@ from . import _lib as L
 from . import ops
 from ._lib import call, ptr
 
+
+# VIT_DORA_SPLITK=0: the factor-gradient GEMMs unsplit (24-32 workgroups each) -- A/B only
+_SPLITK = [os.environ.get("VIT_DORA_SPLITK", "1") != "0"]
 
 class _DoraWeightFn(torch.autograd.Function):
     @staticmethod
@@ -50,9 +54,12 @@ class _DoraWeightFn(torch.autograd.Function):
         dm = torch.empty_like(m)
         dA = torch.empty_like(A)
         dB = torch.empty_like(Bm)
-        ws = ops.workspace("dora_sdDnT", fout * fin * 4, dev)
-        call("vit_dora_weight_bwd", fin, fout, r, ptr(m), ptr(A), ptr(Bm), ptr(gW), ptr(DnT), float(ctx.scaling),
-             ptr(nu), ptr(dm), ptr(dA), ptr(dB), ptr(ws), ptr(nz), L.stream_ptr(dev))
+        # sdDnT [out, in] f32, then the split-K slabs of the two factor GEMMs (16-B aligned)
+        slab_floats = 2 * 256 * 1024 if _SPLITK[0] else 0
+        base = -(-fout * fin // 4) * 4
+        ws = ops.workspace("dora_sdDnT", (base + slab_floats) * 4, dev).view(torch.float32)
+        call("vit_dora_weight_bwd_ws", fin, fout, r, ptr(m), ptr(A), ptr(Bm), ptr(gW), ptr(DnT), float(ctx.scaling),
+             ptr(nu), ptr(dm), ptr(dA), ptr(dB), ptr(ws), ptr(ws[base:]), slab_floats, ptr(nz), L.stream_ptr(dev))
         return dm, dA, dB, None, None, None
 
 

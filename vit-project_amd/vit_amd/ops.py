@@ -554,9 +554,22 @@ def mse_bwd(pred, target, grad_loss=None):
     return d
 
 
+# VIT_GEMM_SPLITK_SMALL=0: small f32 GEMMs (CLIP-HBA's pooled head / logits, < 128 tiles of 32 x 32 over
+# reductions >= 256) unsplit on the generic kernel -- A/B only
+_SPLITK_SMALL = [os.environ.get("VIT_GEMM_SPLITK_SMALL", "1") != "0"]
+
+
 def gemm(P, p_layout, Q, q_layout, M, N, R, out=None, out_dtype=torch.float32, bias=None):
     """Raw C[i][j] = sum_r P(i,r) Q(j,r) (+bias[j]); layouts L.LAY_RC (r contiguous) / L.LAY_CR."""
     assert P.dtype == Q.dtype and P.stride(-1) == 1 and Q.stride(-1) == 1
+    if (_SPLITK_SMALL[0] and out is None and bias is None and P.dtype == torch.float32 and out_dtype == torch.float32
+            and R >= 256 and ((M + 31) // 32) * ((N + 31) // 32) < 128):
+        # few output tiles over a long reduction: split it (vit_gemm_splitk, slab sum in a fixed order)
+        out = torch.empty(M, N, dtype=torch.float32, device=P.device)
+        ws = workspace(f"gemm_splitk:{_s(P)}", 2 * 256 * 1024 * 4, P.device).view(torch.float32)
+        call("vit_gemm_splitk", p_layout, q_layout, M, N, R, ptr(P), P.stride(0), ptr(Q), Q.stride(0), ptr(out),
+             ptr(ws), ws.numel(), _s(P))
+        return out
     if out is None:
         out = torch.empty(M, N, dtype=out_dtype, device=P.device)
     if P.dtype == torch.float32:
