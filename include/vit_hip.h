@@ -244,9 +244,13 @@ int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, 
 int vit_dora_weight_bwd(int in, int out, int r, const float* m, const float* A, const float* B, const float* gW,
                         const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
                         float* sdDnT_ws, const float* noise, void* stream);
-/* ABI 7: the same with a split-K slab workspace (slab_floats >= 2 * 256 * 1024 lets every factor GEMM split;
- * nullptr / 0 = unsplit), and the split-K GEMM it uses: C [M][N] contiguous f32 = sum_r P(i,r) Q(j,r) in
- * r-chunks of >= 128 summed in chunk order (deterministic). */
+/* ABI 7: the same with a split-K slab workspace (nullptr / 0 = unsplit), and the split-K GEMM it uses:
+ * C [M][N] contiguous f32 = sum_r P(i,r) Q(j,r) in r-chunks of >= 128 summed in chunk order
+ * (deterministic).  Slab contract (both functions): the split s is the largest with s <= 256 / tiles,
+ * s <= R / 128 and s * M * N <= slab_floats, and the kernel writes at most s slabs of M * N floats
+ * (chunks of ceil(R / s) rows); s < 2 runs unsplit.  DoRA's factor GEMMs are [in x r] and [r x out],
+ * so 2 * max(in, out) * r floats allow a split of 2 and 2 * 256 * 1024 (the Python callers) their
+ * full split at C3's in = out = 1024, r = 32. */
 int vit_dora_weight_bwd_ws(int in, int out, int r, const float* m, const float* A, const float* B, const float* gW,
                            const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
                            float* sdDnT_ws, float* slabs, int64_t slab_floats, const float* noise, void* stream);

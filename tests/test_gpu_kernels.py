@@ -202,6 +202,38 @@ def test_linear_wgrad_pair_matches_separate(M, tail):
     _close(ob, rb_, 2e-5, "pair b")
 
 
+@pytest.mark.parametrize("M,N,K,split", [(6304, 256, 128, 3), (197 * 64, 768, 3072, 5), (197 * 32, 2304, 768, 2),
+                                         (4096, 640, 448, 1)])
+def test_w4_wgrad_bitwise_matches_pingpong(M, N, K, split):
+    """The wide-wave weight-gradient kernel (w4, round 5's default: 4 waves of 128x128, asm MFMAs on AGPR
+    accumulators) sums every split chunk's k-steps in the same order with the same MFMA as the round-1..4
+    ping-pong kernel (variant 8), so the two agree bit for bit -- odd k-step counts (6304 rows in 3 chunks:
+    66 / 66 / 65 steps), ragged output tiles (640 x 448) and every ring / load-placement configuration
+    (12-15) included; and the pair launch equals two single launches."""
+    lib = L.lib()
+    dy = _rnd(M, N, seed=70, dtype=torch.bfloat16).to(DEV)
+    x = _rnd(M, K, seed=71, dtype=torch.bfloat16).to(DEV)
+    outs = {}
+    try:
+        for v in (8, 11, 12, 13, 14, 15):
+            lib.vit_gemm_variant(v)
+            outs[v] = ops.linear_wgrad(dy, x, split=split).cpu()
+    finally:
+        lib.vit_gemm_variant(-1)
+    ref = dy.float().cpu().T @ x.float().cpu()
+    _close(outs[11], ref, 2e-5, "w4 wgrad")
+    for v in (11, 12, 13, 14, 15):
+        assert torch.equal(outs[v], outs[8]), f"variant {v} differs from the ping-pong kernel"
+    if M % 32 == 0:
+        b = ops.ColBatch()
+        oa, ob = torch.empty(N, K, device=DEV), torch.empty(K, N, device=DEV)
+        ops.linear_wgrad_pair((dy, x, oa), (x, dy, ob), b)
+        b.launch()
+        torch.cuda.synchronize()
+        _close(oa, ref, 2e-5, "pair a")
+        _close(ob, ref.T, 2e-5, "pair b")
+
+
 @pytest.mark.parametrize("group", [1, 3, 8])
 def test_gemm_grouped_tile_walk(group):
     """The banded tile walk (vit_gemm_group) is a bijection over the tiles: every output tile is
@@ -220,7 +252,7 @@ def test_gemm_grouped_tile_walk(group):
         lib.vit_gemm_group(0, 0)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
 def test_gemm_every_tile_config(variant):
     """Every kept MFMA configuration (forced through vit_gemm_variant) on ragged
     M/N tiles, fwd + bias/GELU/residual epilogues, dgrad, split-K wgrad."""
@@ -504,6 +536,29 @@ def test_gemm_splitk_matches_reference(M, N, R):
             _close(outs[0], ref, 1e-5, f"splitk {pl}{ql}")
             _close(outs[2], ref, 1e-5, f"unsplit {pl}{ql}")
             assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("R", [1025, 1100, 2047])
+def test_gemm_splitk_slab_room_exact(R):
+    """a reduction that is not a multiple of split * 64 with exactly split * M * N floats of slab
+    room (M = N = 32: one tile, split min(256, R / 128) = 8).  The kernel must write at most `split` slabs
+    (chunks of ceil(R / split) rows), so a guard region right after the room stays untouched."""
+    lib = L.lib()
+    st = torch.cuda.current_stream().cuda_stream
+    M = N = 32
+    split = min(256, R // 128)
+    room = split * M * N
+    g = torch.Generator().manual_seed(R)
+    Pm, Qm = torch.randn(M, R, generator=g), torch.randn(N, R, generator=g)
+    buf = torch.full((room + 4096,), 12345.0, device=DEV)
+    c = torch.empty(M, N, device=DEV)
+    Pd, Qd = Pm.to(DEV), Qm.to(DEV)
+    rc = lib.vit_gemm_splitk(L.LAY_RC, L.LAY_RC, M, N, R, Pd.data_ptr(), R, Qd.data_ptr(), R, c.data_ptr(),
+                             buf.data_ptr(), room, st)
+    assert rc == 0, rc
+    torch.cuda.synchronize()
+    assert bool((buf[room:] == 12345.0).all()), "split-K slabs overran slab_floats"
+    _close(c.cpu(), (Pm.double() @ Qm.double().t()).float(), 1e-5, f"splitk R={R}")
 
 
 # ---------------------------------------------------------------------------- LayerNorm

@@ -30,6 +30,7 @@ from step_classes import classify  # noqa: E402
 
 LABELS = [  # (regex on the mangled name, label)
     (r"pp_kernel", "wgrad: split-K ping-pong 256x256x32 (every dW)"),
+    (r"w47kernel2|w4::kernel2|_ZN2w46kernelINS_3CfgI(?:Li\d+E)+EELi1ELi1E", "wgrad: w4 4-wave 256x256x32 (every dW)"),
     (r"splitk_reduce", "wgrad: split-K slab reduce"),
     (r"CfgILi256ELi256ELi64E.*ELi0ELi0ELi0E", "fwd: V5 256x256x64 plain bf16 (qkv, fc2)"),
     (r"CfgILi256ELi256ELi64E.*ELi0ELi0ELi1E", "fwd: V5 256x256x64 bias+GELU pair (fc1)"),

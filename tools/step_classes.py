@@ -30,11 +30,18 @@ FLOP = {
     "attention bwd": 12 * 10 * B * H * N * N * 64,
 }
 _CFG = re.compile(r"gemm_kernelINS_3CfgI(?:L[ib]\d+E)+EELi(\d)ELi(\d)E")
+# the wide-wave kernels (csrc/gemm_w4.inc, round 5): the pair launch is always a weight gradient; the
+# single launch's layout pair is its 2nd / 3rd template argument (mangled or demangled)
+_W4 = re.compile(r"_ZN2w46kernelINS_3CfgI(?:Li\d+E)+EELi(\d)ELi(\d)E|w4::kernel<w4::Cfg<\d+, \d+>, (\d), (\d),")
 
 
 def classify(name: str) -> str:
-    if "pp_kernel" in name or "splitk_reduce" in name:
+    if "pp_kernel" in name or "splitk_reduce" in name or "w47kernel2" in name or "w4::kernel2" in name:
         return "gemm wgrad"
+    w = _W4.search(name)
+    if w:
+        pl, ql = (int(w.group(1)), int(w.group(2))) if w.group(1) else (int(w.group(3)), int(w.group(4)))
+        return {(0, 0): "gemm fwd", (0, 1): "gemm dgrad", (1, 1): "gemm wgrad"}.get((pl, ql), "gemm other")
     m = _CFG.search(name)
     if m or "pers" in name and "gemm_kernel" in name:
         pl, ql = (int(m.group(1)), int(m.group(2))) if m else (0, 0)

@@ -152,8 +152,9 @@ int vit_dora_weight_fwd(int in, int out, int r, const float* m, const float* A, 
 
 // Backward of vit_dora_weight_fwd given gW = dL/dW [out, in]; DnT/nu from the forward.
 // sdDnT_ws >= out*in floats.  Outputs dm [out], dA [r, out], dB [in, r] (f32, overwritten).
-// ABI 7: slabs / slab_floats (>= 2 * max(in, out) * r floats to split) let the two factor GEMMs split their
-// 1024-4096-long reductions (vit_gemm_splitk); nullptr / 0 = the unsplit launches of vit_dora_weight_bwd.
+// ABI 7: slabs / slab_floats let the two factor GEMMs split their 1024-4096-long reductions
+// (vit_gemm_splitk; slab contract in include/vit_hip.h: at most s slabs of M * N floats with
+// s * M * N <= slab_floats); nullptr / 0 = the unsplit launches of vit_dora_weight_bwd.
 int vit_dora_weight_bwd_ws(int in, int out, int r, const float* m, const float* A, const float* Bm, const float* gW,
                            const float* DnT, float scaling, const float* nu, float* dm, float* dA, float* dB,
                            float* sdDnT_ws, float* slabs, int64_t slab_floats, const float* noise, void* stream) {

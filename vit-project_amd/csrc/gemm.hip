@@ -1144,6 +1144,7 @@ using V7 = Cfg<128, 256, 32, 2, 2, 3, false, 2, 1>;  // 4 waves of 64x128
 
 #include "pgemm.inc"
 #include "gemm_f32.inc"
+#include "gemm_w4.inc"
 
 // ----------------------------------------------------------------------------
 // Generic strided kernel: any M, N, R; f32 or bf16 inputs; fp32 FMA.
@@ -1319,7 +1320,7 @@ static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool per
   int v;
   if (g_variant >= 0) v = g_variant % 100;
   else if (o >= 0) v = o;
-  else if (wgrad) v = 8;                                                   // wgrad: ping-pong 256x256
+  else if (wgrad) v = 11;  // wgrad: 4 waves of 128x128 (w4, round 5; 8 = the round-1..4 ping-pong kernel)
   else if (fwd && act_fwd && o_fwd_gelu >= 0) v = o_fwd_gelu;               // forward with the GELU pair
   else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : (o_fwd_small >= 0 ? o_fwd_small : 5);  // forward
   // (the N, R < 1536 forwards -- proj, patch embedding -- moved from V2 to V5 in round 3: +0.35 % step,
@@ -1333,8 +1334,13 @@ static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool per
   return v;
 }
 
+// rows per split-K chunk: ceil(R / split) rounded up to the k-step, so the launch never has more
+// than `split` chunks (nz = ceil(R / r_chunk) <= split): every slab-size check against split * M * N
+// then covers the slabs the kernel writes (R = 1025, split = 8: 192-row chunks, 6 slabs -- the
+// floor(R / split) rounding gave 128 and 9 slabs)
 static int r_chunk_for(int R, int split, int bk) {
-  int c = ((R / split + bk - 1) / bk) * bk;
+  if (split < 1) split = 1;
+  int c = (((R + split - 1) / split + bk - 1) / bk) * bk;
   return c > 0 ? c : bk;
 }
 
@@ -1375,6 +1381,25 @@ static int launch_pp(const void* P, int64_t ldp, const void* Q, int64_t ldq, int
   dim3 grid(((M + 255) / 256) * ((N + 255) / 256) * nz);
   hipLaunchKernelGGL((big::pp_kernel<S, PL, QL, EPI, TO, TA>), grid, dim3(C::THREADS), C::LDS, s,
                      (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, r_chunk, e);
+  VIT_CHECK_LAUNCH();
+  return 0;
+}
+
+template <class C, int PL, int QL, int EPI, typename TO, typename TA>
+static int launch_w4(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
+                     const Epi& e, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)w4::kernel<C, PL, QL, EPI, TO, TA>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+    attr = true;
+  }
+  if (R % w4::BK) return (int)hipErrorInvalidValue;
+  const int r_chunk = r_chunk_for(R, split, 64);
+  const int nz = (R + r_chunk - 1) / r_chunk;
+  dim3 grid(((M + 255) / 256) * ((N + 255) / 256) * nz);
+  hipLaunchKernelGGL((w4::kernel<C, PL, QL, EPI, TO, TA>), grid, dim3(C::THREADS), C::LDS, s, (const bf16*)P, ldp,
+                     (const bf16*)Q, ldq, M, N, R, r_chunk, e);
   VIT_CHECK_LAUNCH();
   return 0;
 }
@@ -1439,6 +1464,12 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
       return launch_pers<PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, e, s);
     if (v == 10) return launch_big<big::V1, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
   }
+  if constexpr (PL == LAY_CR && QL == LAY_CR) {  // w4 ring / load-placement A/B (tools/bench_kernels.py --sweep)
+    if (v == 12) return launch_w4<w4::Cfg<4, 0>, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    if (v == 13) return launch_w4<w4::Cfg<4, 2>, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    if (v == 14) return launch_w4<w4::Cfg<3, 1>, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    if (v == 15) return launch_w4<w4::Cfg<5, 1>, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+  }
   switch (v) {
     case 2: return launch_big<big::V2, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 5: return launch_big<big::V5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
@@ -1448,6 +1479,7 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
     case 7: return launch_big<big::V7, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 8: return launch_pp<4, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     case 9: return launch_pp<5, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
+    case 11: return launch_w4<w4::Default, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     default: return launch_big<big::V1, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
   }
 }
@@ -1517,8 +1549,7 @@ static int launch_f32(const void* P, int64_t ldp, const void* Q, int64_t ldq, in
 template <typename T, int EPI, typename TO, typename TA>
 static int launch_gen(const void* P, int64_t sPi, int64_t sPr, const void* Q, int64_t sQj, int64_t sQr,
                       int M, int N, int R, int split, const Epi& e, hipStream_t s) {
-  int r_chunk = ((R / split + gen::TK - 1) / gen::TK) * gen::TK;
-  if (r_chunk <= 0) r_chunk = gen::TK;
+  const int r_chunk = r_chunk_for(R, split, gen::TK);
   int nz = (R + r_chunk - 1) / r_chunk;
   if (nz == 0) nz = 1;
   const int64_t big_tiles = (int64_t)((N + 63) / 64) * ((M + 63) / 64) * nz;
@@ -1927,15 +1958,28 @@ int vit_linear_wgrad_partials2(int M, int split, int Na, int Ka, const void* dYa
     return p;
   };
   const big::PPProb a = prob(dYa, lddya, Xa, ldxa, Na, Ka, slabs_a), b = prob(dYb, lddyb, Xb, ldxb, Nb, Kb, slabs_b);
-  using C = big::PP<4>;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-    attr = true;
+  // the weight-gradient kernel pick_variant chooses (11 = w4, 8 = the ping-pong kernel; VIT_GEMM_WGRAD A/B)
+  if (pick_variant(LAY_CR, LAY_CR, Na, Ka, M, split, false, false) == 8) {
+    using C = big::PP<4>;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL((big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>), dim3(a.nwg + b.nwg),
+                       dim3(C::THREADS), C::LDS, s, a, b);
+  } else {
+    using C = w4::Default;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)w4::kernel2<C, LAY_CR, LAY_CR, EPI_STORE, float, bf16>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+      attr = true;
+    }
+    hipLaunchKernelGGL((w4::kernel2<C, LAY_CR, LAY_CR, EPI_STORE, float, bf16>), dim3(a.nwg + b.nwg),
+                       dim3(C::THREADS), C::LDS, s, a, b);
   }
-  hipLaunchKernelGGL((big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>), dim3(a.nwg + b.nwg),
-                     dim3(C::THREADS), C::LDS, s, a, b);
   VIT_CHECK_LAUNCH();
   return 0;
 }
