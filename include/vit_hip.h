@@ -35,7 +35,8 @@ enum {
   VIT_EPI_QGELU_BWD = 6
 };
 
-int vit_abi_version(void);
+int vit_abi_version(void); /* 8 (round 5): vit_gemm_ms / vit_gemm_ms_config and the banded attention
+                              * backward removed; the weight-gradient GEMMs on the w4 kernel */
 
 /* Generic MFMA GEMM C[i][j] = epi(sum_r P(i,r) Q(j,r)); layouts RC (r contiguous)
  * or CR (i/j contiguous).  Backs every nn.Linear of timm's ViT reached from
@@ -51,21 +52,6 @@ int vit_gemm_variant(int v);
  * row tiles, column-major inside a band (L2 reuse of the weight columns); 0 = row-major (the
  * default), -1 = the per-shape rule (bands of 8 for wide outputs with >= 4 MiB weights). */
 int vit_gemm_group(int fwd, int dgrad);
-
-/* Multi-tile bf16 GEMM with deferred stores (csrc/gemm_ms.hip): a workgroup runs tiles w, w + grid, ...
- * and issues each tile's 16-B stores under the next tile's MFMAs.  Y[M,N] = X[M,K] W^T (+ bias), bf16 in
- * and out; wl = 0: W [N][K] (the F.linear forwards of VIT:139, qkv / proj / fc1 / fc2), wl = 1: W [K][N]
- * (the plain input gradients dX = dY W of VIT:142).  epi 0 = store, 1 = the GELU pair of
- * VIT_EPI_BIAS_GELU (C = gelu'(pre), C2 = gelu(pre); wl = 0).  cfg 0-3 = row tile (192 / 256) and how
- * many of a tile's stores are deferred into the next tile's k-steps (csrc/gemm_ms.hip).  Opt-in route
- * for vit_linear_fwd / vit_linear_dgrad (vit_gemm_ms_config); hipErrorInvalidValue for shapes outside
- * its contract (N % 256, K % 64).  Bit-identical to the one-tile kernels. */
-int vit_gemm_ms(int epi, int wl, int cfg, int M, int N, int K, const void* X, int64_t ldx, const void* W,
-                int64_t ldw, const float* bias, void* C, int64_t ldc, void* C2, int grid, void* stream);
-/* Tuning hook: the multi-tile route's class mask (1 = forwards, 2 = input gradients, 0 = off, the
- * default; < 0 keeps it), its cfg (< 0 keeps it), tiles per workgroup (< 1 keeps it); defaults from
- * VIT_GEMM_MS, VIT_GEMM_MS_CFG, VIT_GEMM_MS_T. */
-int vit_gemm_ms_config(int on, int cfg, int tiles_per_wg);
 
 /* Stream-K workspace for the fp32 MFMA GEMMs launched on `stream` (the reference-precision C3 path,
  * NEWP:274): part >= 4 * CUs * 128*128 floats, counters >= 2 * CUs ints, zero-filled before first use
@@ -214,9 +200,9 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
                  float* delta_ws, float scale, int causal, float* dbias, float* partial, int64_t partial_floats,
                  void* stream);
 int vit_sdpa_bwd_partial_floats(int B, int N, int D);
-/* Tuning hook: the bf16 backward form for N <= 224 (-1 = from VIT_ATTN_BWD_BAND / VIT_ATTN_BWD_SPLIT,
- * 0 = banded queries (N > 112; opt-in, measured slower), 1 = whole-head fused (the default), 2 = two
- * kernels).  All forms give bit-identical dq / dk / dv. */
+/* Tuning hook: the bf16 backward form for N <= 224 (-1 = from VIT_ATTN_BWD_SPLIT, 1 = whole-head fused
+ * (the default), 2 = two kernels; 0, round 4's banded form, was removed in ABI 8: hipErrorInvalidValue).
+ * Both forms give bit-identical dq / dk / dv. */
 int vit_sdpa_bwd_variant(int v);
 
 /* torch.nn.functional.cross_entropy(outputs, targets) mean (VIT:140) and its gradient. */

@@ -252,7 +252,7 @@ def test_gemm_grouped_tile_walk(group):
         lib.vit_gemm_group(0, 0)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15])
+@pytest.mark.parametrize("variant", [1, 2, 3, 4, 5, 6, 7, 8, 9, 11, 12, 13, 14, 15])
 def test_gemm_every_tile_config(variant):
     """Every kept MFMA configuration (forced through vit_gemm_variant) on ragged
     M/N tiles, fwd + bias/GELU/residual epilogues, dgrad, split-K wgrad."""
@@ -359,46 +359,6 @@ def test_f32_gemm_streamk_matches_reference(M, N, K):
         _close(plain, y1, 1e-6, "plain vs stream-K")
     finally:
         O._streamk(torch.device(DEV))
-
-
-@pytest.mark.parametrize("K", [448, 768])
-def test_gemm_persistent_many_tiles(K):
-    """The persistent forward / dgrad kernel (variant 10) with more tiles than CUs, so the
-    workgroups run several tiles each (deferred stores, dynamic tile hand-out, stealing,
-    counter reset), a ragged last row tile (buffer range check drops rows >= M) and
-    k-loops shorter (K = 448) and longer than the store schedule; every epilogue, twice
-    in a row (the second launches reuse the reset counter slots)."""
-    lib = L.lib()
-    M, N = 197 * 96 + 5, 640          # 74 row tiles x 5 column tiles = 370 tiles > 256 CUs
-    x = _rnd(M, K, seed=50, dtype=torch.bfloat16)
-    w = _rnd(N, K, seed=51, scale=0.05, dtype=torch.bfloat16)
-    b = _rnd(N, seed=52)
-    res = _rnd(M, N, seed=53)
-    dy = _rnd(M, N, seed=54, dtype=torch.bfloat16)
-    dact = _rnd(M, K, seed=55, dtype=torch.bfloat16)
-    xd, wd, bd, dyd, dad = x.to(DEV), w.to(DEV), b.to(DEV), dy.to(DEV), dact.to(DEV)
-    ref = x.float() @ w.float().T + b
-    dref = dy.float() @ w.float()
-    lib.vit_gemm_variant(10)
-    try:
-        for _ in range(2):
-            _close(ops.linear_fwd(xd, wd, bd, out_dtype=torch.bfloat16), ref, 1e-2, "store bf16")
-            _close(ops.linear_fwd(xd, wd, bd, out_dtype=torch.float32), ref, 1e-5, "store f32")
-            da, act = ops.linear_fwd(xd, wd, bd, epi=L.EPI_BIAS_GELU)
-            _close(act, torch.nn.functional.gelu(ref), 1e-2, "gelu")
-            _close(da, _gelu_grad(ref), 1e-2, "gelu'")
-            out = res.to(DEV).clone()
-            ops.linear_fwd(xd, wd, bd, epi=L.EPI_RESID, resid=out, out=out)
-            _close(out, ref + res, 1e-5, "resid")
-            db = torch.empty(K, device=DEV)
-            d = ops.linear_dgrad(dyd, wd, out_dtype=torch.bfloat16, epi=L.EPI_GELU_BWD, pre=dad, dbias=db)
-            gref = dref * dact.float()
-            _close(d, gref, 1e-2, "dgrad gelu'")
-            _close(db, gref.sum(0), 1e-3, "dgrad fused bias")
-            _close(ops.linear_dgrad(dyd, wd), dref, 1e-5, "dgrad f32")
-            _close(ops.linear_dgrad(dyd, wd, out_dtype=torch.bfloat16), dref, 1e-2, "dgrad bf16")
-    finally:
-        lib.vit_gemm_variant(-1)
 
 
 def test_gemm_cr_rc_layout_fast():
@@ -744,10 +704,10 @@ def test_sdpa_bwd_large_grid(B, H, N, causal):
 
 @pytest.mark.parametrize("N,causal", [(113, False), (150, False), (197, False), (224, False), (197, True),
                                       (224, True)])
-def test_sdpa_bwd_banded_matches_whole_head(N, causal):
-    """The banded backward (queries streamed in 32-row bands, round 4) against the whole-head fused
-    kernel: dq / dk / dv bit-identical (same MFMA order per output), delta identical, the qkv-bias
-    column sums within fp32 summation-order error; B*H = 300 workgroups (several per CU slot)."""
+def test_sdpa_bwd_fused_matches_two_kernel(N, causal):
+    """The whole-head fused backward (the default for N <= 224) against the two-kernel form (dq kernel +
+    dk/dv kernel, the N > 224 path): dq / dk / dv bit-identical (same MFMA order per output), delta
+    identical, the qkv-bias column sums within fp32 summation-order error; B*H = 300 workgroups."""
     B, H = 25, 12
     D = H * 64
     g = torch.Generator(device=DEV).manual_seed(37)
@@ -757,8 +717,9 @@ def test_sdpa_bwd_banded_matches_whole_head(N, causal):
     lib = L.lib()
     outs = []
     try:
-        for v in (1, 0):
-            lib.vit_sdpa_bwd_variant(v)
+        assert lib.vit_sdpa_bwd_variant(0) != 0  # the banded form is gone (ABI 8)
+        for v in (1, 2):
+            assert lib.vit_sdpa_bwd_variant(v) == 0
             dbias = torch.empty(3 * D, device=DEV)
             dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=dbias, causal=causal)
             delta = ops.workspace("sdpa_delta", B * H * N * 4, qkv.device).view(torch.float32)[:B * H * N].clone()
@@ -769,45 +730,7 @@ def test_sdpa_bwd_banded_matches_whole_head(N, causal):
     (d0, b0, l0), (d1, b1, l1) = outs
     assert torch.equal(d0, d1), (d0.float() - d1.float()).abs().max().item()
     assert torch.equal(l0, l1)
-    _close(b1, b0, 1e-5, "qkv bias grad (banded vs fused)")
-
-
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
-def test_gemm_ms_matches_default(cfg):
-    """The opt-in multi-tile deferred-store GEMM (csrc/gemm_ms.hip, round 4) against the default
-    one-tile path on the same inputs: forward store, forward GELU pair, input gradient (W [K][N]);
-    bit-identical (same k-order per output).  Ragged M (not a multiple of the 192 / 256-row tiles), and
-    a grid smaller than the tile count, so workgroups run several tiles and defer stores across them."""
-    lib = L.lib()
-    lib.vit_gemm_ms_config(0, -1, -1)
-    bf = torch.bfloat16
-    st = torch.cuda.current_stream().cuda_stream
-    M = 1000
-    for K, N, epi, wl in [(768, 2304, 0, 0), (768, 768, 0, 0), (768, 3072, 1, 0), (3072, 768, 0, 1)]:
-        x = _rnd(M, K, seed=K + N, dtype=bf).to(DEV)
-        w = _rnd(*((K, N) if wl else (N, K)), seed=7, scale=0.05, dtype=bf).to(DEV)
-        b = None if wl else _rnd(N, seed=9).to(DEV)
-        y0, y1 = torch.empty(M, N, device=DEV, dtype=bf), torch.empty(M, N, device=DEV, dtype=bf)
-        if wl:
-            ops.linear_dgrad(x, w, out_dtype=bf, out=y0)
-        elif epi:
-            ops.linear_fwd(x, w, b, epi=L.EPI_BIAS_GELU, out=y0, act_out=y1)
-        else:
-            ops.linear_fwd(x, w, b, out=y0)
-        for grid in (0, 7):
-            z0, z1 = torch.zeros_like(y0), torch.zeros_like(y1)
-            rc = lib.vit_gemm_ms(epi, wl, cfg, M, N, K, x.data_ptr(), K, w.data_ptr(), N if wl else K,
-                                 None if b is None else b.data_ptr(), z0.data_ptr(), N,
-                                 z1.data_ptr() if epi else None, grid, st)
-            assert rc == 0, rc
-            torch.cuda.synchronize()
-            assert torch.equal(z0, y0), (K, N, epi, wl, grid, (z0.float() - y0.float()).abs().max().item())
-            if epi:
-                assert torch.equal(z1, y1), (K, N, grid)
-    # outside the contract (N % 256): refused, nothing launched
-    z = torch.empty(M, 200, device=DEV, dtype=bf)
-    assert lib.vit_gemm_ms(0, 0, cfg, M, 200, 768, x.data_ptr(), 768, x.data_ptr(), 768, None, z.data_ptr(),
-                           200, None, 0, st) != 0
+    _close(b1, b0, 1e-5, "qkv bias grad (two-kernel vs fused)")
 
 
 @pytest.mark.parametrize("N", [77, 16, 197, 224])

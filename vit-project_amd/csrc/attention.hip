@@ -926,268 +926,6 @@ __global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_fused(
 }
 
 // ---------------------------------------------------------------------------
-// bf16 backward, banded (8 <= NT <= 14): attn_bwd_fused's arithmetic with the queries streamed.
-// attn_bwd_fused loads the whole head's Q, dO, O (and computes delta) in a prologue that nothing
-// overlaps (one workgroup per CU, 149 KiB of LDS): ~30 % of its time.  Here Q / dO and
-// the row constants pass through LDS in bands of 32 queries (two query tiles), double-buffered:
-// band qp + 2 is fetched into registers while band qp is processed, and written to LDS after band
-// qp + 1's phase 1.  Per band: phase 1 (wave = key tile: S, dP of its keys against the band ->
-// dK, dV, dS^T of the band), one barrier, then dQ of the band (8 waves, one (query tile, d-tile)
-// fragment each, over every key) while the other waves go on to the next band.  LDS 74 KiB at
-// N = 197 (K image for dQ, 2 x band images, 2 x dS^T bands).  dq / dk / dv are bit-identical to
-// attn_bwd_fused (same MFMA order per output); only the qkv-bias column sums of dq are summed in
-// another order.
-// ---------------------------------------------------------------------------
-template <int NT> struct BwdB {
-  static constexpr int NT2 = (NT + 1) / 2, ROWS = NT2 * 32, THREADS = NT * 64;
-  static constexpr int KIMG = ROWS * 128;       // K rows (dQ's operand), padded keys zero
-  static constexpr int BIMG = 32 * 128;         // one band of Q or dO rows
-  static constexpr int BSET = 2 * BIMG + 2 * 32 * 4;  // Q, dO images + -lse/scale, -delta of the band
-  static constexpr int DSB = 2 * ROWS * 32;     // dS^T of a band: 2 query tiles x [ROWS keys][16 q] bf16
-  static constexpr int LDS = KIMG + 2 * BSET + 2 * DSB;
-  static constexpr int RED = (3 * NT + 8) * 64 * 4;  // bias-partial reduction (reuses the LDS)
-  static_assert(RED <= LDS && NT >= 8 && NT <= 14, "banded backward shape");
-};
-
-template <int NT, bool CAUSAL = false>
-__global__ __launch_bounds__(NT * 64, (NT + 3) / 4) void attn_bwd_band(
-    const bf16* __restrict__ qkv, int64_t ld_qkv, int D, int H, int N, float scale, const bf16* __restrict__ o,
-    int64_t ld_o, const bf16* __restrict__ dout, int64_t ld_do, const float* __restrict__ lse,
-    float* __restrict__ delta_out, bf16* __restrict__ dqkv, int64_t ld_dqkv, float* __restrict__ bias_part) {
-  using F = BwdB<NT>;
-  constexpr int NT2 = F::NT2, ROWS = F::ROWS, NTHR = F::THREADS;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Kimg = smem;
-  auto bset = [&](int buf) { return smem + F::KIMG + buf * F::BSET; };  // Q image, dO image, lse2[32], delta[32]
-  auto dsb = [&](int buf) { return smem + F::KIMG + 2 * F::BSET + buf * F::DSB; };
-  const int bh = blockIdx.x, b = bh / H, h = bh - b * H;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l15 = lane & 15;
-  const bf16* base = qkv + (int64_t)b * N * ld_qkv + h * 64;
-  const bf16* dob = dout + (int64_t)b * N * ld_do + h * 64;
-  const bf16* obase = o + (int64_t)b * N * ld_o + h * 64;
-
-  // ---- band prefetch: slots [0, 256) carry a dO + O chunk (delta), [256, 512) a Q chunk (+ lse)
-  constexpr int PER = (512 + NTHR - 1) / NTHR;
-  bf16x8 pa[PER], pb[PER];
-  float pl[PER];
-  auto fetch = [&](int band) {
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int idx = tid + u * NTHR;
-      const int j = idx & 255, row = min(band * 32 + (j >> 3), N - 1), c = j & 7;
-      if (idx < 256) {
-        pa[u] = *reinterpret_cast<const bf16x8*>(dob + (int64_t)row * ld_do + c * 8);
-        pb[u] = *reinterpret_cast<const bf16x8*>(obase + (int64_t)row * ld_o + c * 8);
-      } else if (idx < 512) {
-        pa[u] = *reinterpret_cast<const bf16x8*>(base + (int64_t)row * ld_qkv + c * 8);
-        if (c == 0) pl[u] = lse[(int64_t)bh * N + row];
-      }
-    }
-  };
-  auto commit = [&](int band, int buf) {
-    char* Qb = bset(buf);
-    char* Ob = Qb + F::BIMG;
-    float* lse2 = reinterpret_cast<float*>(Qb + 2 * F::BIMG);
-    float* delta = lse2 + 32;
-#pragma unroll
-    for (int u = 0; u < PER; ++u) {
-      const int idx = tid + u * NTHR;  // wave-uniform ranges: NTHR and 256 are multiples of 64
-      const int j = idx & 255, r = j >> 3, c = j & 7, row = band * 32 + r;
-      const bool live = row < N;
-      if (idx < 256) {
-        float dl = 0.f;
-        if (live) {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) dl = fmaf((float)pa[u][e], (float)pb[u][e], dl);
-        }
-        dl += __shfl_xor(dl, 1, 64);
-        dl += __shfl_xor(dl, 2, 64);
-        dl += __shfl_xor(dl, 4, 64);
-        bf16x8 w = pa[u];
-        if (!live) {
-#pragma unroll
-          for (int t = 0; t < 8; ++t) w[t] = (bf16)0.f;
-        }
-        *reinterpret_cast<bf16x8*>(Ob + at_off(r, c)) = w;
-        if (c == 0) {
-          delta[r] = -dl;
-          if (live) delta_out[(int64_t)bh * N + row] = dl;
-        }
-      } else if (idx < 512) {
-        bf16x8 w = pa[u];
-        if (!live) {
-#pragma unroll
-          for (int t = 0; t < 8; ++t) w[t] = (bf16)0.f;
-        }
-        *reinterpret_cast<bf16x8*>(Qb + at_off(r, c)) = w;
-        if (c == 0) lse2[r] = live ? -pl[u] / scale : -INFINITY;
-      }
-    }
-  };
-
-  // ---- prologue: this wave's key tile (registers and the K image), band 0, band 1 in flight
-  const int key = wave * 16 + l15;
-  const bool kvalid = key < N;
-  bf16x8 kf[2], vf[2];
-  {
-    const int kc = min(key, N - 1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      kf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)kc * ld_qkv + D + kk * 32 + g * 8);
-      vf[kk] = *reinterpret_cast<const bf16x8*>(base + (int64_t)kc * ld_qkv + 2 * D + kk * 32 + g * 8);
-    }
-  }
-  fetch(0);
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    bf16x8 w = kf[kk];
-    if (!kvalid) {
-#pragma unroll
-      for (int t = 0; t < 8; ++t) w[t] = (bf16)0.f;
-    }
-    *reinterpret_cast<bf16x8*>(Kimg + at_off(key, kk * 4 + g)) = w;
-  }
-  {
-    // K rows and dS^T rows of the padded keys [NT*16, ROWS) (read by the last key pair of dQ): zero
-    constexpr int PADK = (ROWS - NT * 16) * 8, PADS = (ROWS - NT * 16) * 32 / 16;
-    if constexpr (PADK > 0) {
-      for (int i = tid; i < PADK; i += NTHR)
-        *reinterpret_cast<f32x4*>(Kimg + (NT * 16) * 128 + i * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int i = tid; i < 4 * PADS; i += NTHR) {
-        const int t = i / PADS, r = i - t * PADS;  // (buffer, query tile) pair t
-        *reinterpret_cast<f32x4*>(dsb(t >> 1) + (t & 1) * ROWS * 32 + NT * 16 * 32 + r * 16) =
-            f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-  }
-  commit(0, 0);
-  if (NT2 > 1) fetch(1);
-  const AtOffsets off(lane);
-  __syncthreads();
-  const float c2 = scale * LOG2E;
-
-  f32x4 dv[4], dk[4];
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) { dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f}; dk[dt] = dv[dt]; }
-  f32x4 csq = f32x4{0.f, 0.f, 0.f, 0.f};  // dQ waves: column partial sums of their dq fragment
-  const int fq = wave >> 2, fdt = wave & 3;  // dQ waves (wave < 8): query tile of the band, d-tile
-#pragma unroll 1
-  for (int qp = 0; qp < NT2; ++qp) {
-    const int cur = qp & 1;
-    const char* Qc = bset(cur);
-    const char* Oc = Qc + F::BIMG;
-    const float* lse2 = reinterpret_cast<const float*>(Qc + 2 * F::BIMG);
-    const float* delta = lse2 + 32;
-    char* dsw = dsb(cur) + key * 32 + g * 8;
-    // ---- phase 1 (this wave's key tile against the band's two query tiles)
-    f32x4 p[2], ds[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int qt = 2 * qp + u;
-      const f32x4 nl = *reinterpret_cast<const f32x4*>(lse2 + u * 16 + 4 * g);
-      f32x4 sacc = kvalid ? nl : f32x4{-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-      f32x4 dpacc = *reinterpret_cast<const f32x4*>(delta + u * 16 + 4 * g);
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        sacc = mfma16(rowf(Qc, u * 16, off.row[kk]), kf[kk], sacc);
-        dpacc = mfma16(rowf(Oc, u * 16, off.row[kk]), vf[kk], dpacc);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float pv = fexp2(sacc[r] * c2);
-        if constexpr (CAUSAL) { if (key > qt * 16 + 4 * g + r) pv = 0.f; }
-        p[u][r] = pv;
-        ds[u][r] = pv * dpacc[r];
-      }
-      if (qt < NT) {
-        const bf16x4 w = {(bf16)ds[u][0], (bf16)ds[u][1], (bf16)ds[u][2], (bf16)ds[u][3]};
-        *reinterpret_cast<bf16x4*>(dsw + u * ROWS * 32) = w;
-      }
-    }
-    const bf16x8 pf = pack8(p[0], p[1]), dsf = pack8(ds[0], ds[1]);
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dv[dt] = mfma16(trf(Oc, 0, off.tr[dt]), pf, dv[dt]);
-      dk[dt] = mfma16(trf(Qc, 0, off.tr[dt]), dsf, dk[dt]);
-    }
-    // ---- band qp + 1 into the other buffer set (its last readers finished before the previous
-    // barrier), band qp + 2 on its way into registers
-    if (qp + 1 < NT2) {
-      commit(qp + 1, cur ^ 1);
-      if (qp + 2 < NT2) fetch(qp + 2);
-    }
-    __syncthreads();  // dS^T of the band complete; band qp + 1 visible
-    // ---- dQ of the band: wave (fq, fdt) < 8, all keys (the key pairs of attn_bwd_fused's phase 2)
-    const int qt = 2 * qp + fq;
-    if (wave < 8 && qt < NT) {
-      const char* dsr = dsb(cur) + fq * ROWS * 32 + (4 * g + (l15 >> 2)) * 32 + (l15 & 3) * 8;
-      f32x4 dq = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int kp = 0; kp < NT2; ++kp) {
-        const bf16x8 sf = cat4(lds_read_tr(dsr + kp * 32 * 32), lds_read_tr(dsr + kp * 32 * 32 + 16 * 32));
-        dq = mfma16(trf(Kimg, kp * 32, off.tr[fdt]), sf, dq);
-      }
-      const int q = qt * 16 + l15;
-      dq = q < N ? dq * scale : f32x4{0.f, 0.f, 0.f, 0.f};
-      if (q < N) {
-        const bf16x4 qv4 = {(bf16)dq[0], (bf16)dq[1], (bf16)dq[2], (bf16)dq[3]};
-        *reinterpret_cast<bf16x4*>(dqkv + ((int64_t)b * N + q) * ld_dqkv + h * 64 + fdt * 16 + 4 * g) = qv4;
-      }
-      csq += dq;
-    }
-  }
-#pragma unroll
-  for (int dt = 0; dt < 4; ++dt) {
-    dk[dt] = kvalid ? dk[dt] * scale : f32x4{0.f, 0.f, 0.f, 0.f};
-    if (!kvalid) dv[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  if (kvalid) {
-    bf16* row = dqkv + ((int64_t)b * N + key) * ld_dqkv + h * 64;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      bf16x4 kv = {(bf16)dk[dt][0], (bf16)dk[dt][1], (bf16)dk[dt][2], (bf16)dk[dt][3]};
-      bf16x4 vv = {(bf16)dv[dt][0], (bf16)dv[dt][1], (bf16)dv[dt][2], (bf16)dv[dt][3]};
-      *reinterpret_cast<bf16x4*>(row + D + dt * 16 + 4 * g) = kv;
-      *reinterpret_cast<bf16x4*>(row + 2 * D + dt * 16 + 4 * g) = vv;
-    }
-  }
-  if (bias_part) {  // dk, dv: [2][NT][64] compressed partials; dq: [8][64] fragment-column partials
-    float* red = reinterpret_cast<float*>(smem);
-    float* redq = red + 3 * NT * 64;
-    const float ck = colsum16(dk, lane), cv = colsum16(dv, lane);
-    float own = 0.f;  // dq: lane l15 = t of group g owns column fdt * 16 + 4g + t
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      float v = csq[t];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      if (l15 == t) own = v;
-    }
-    __syncthreads();  // the last band's dQ reads of the LDS are done
-    for (int i = tid; i < 8 * 64; i += NTHR) redq[i] = 0.f;
-    __syncthreads();
-    red[(1 * NT + wave) * 64 + colsum16_col(lane)] = ck;
-    red[(2 * NT + wave) * 64 + colsum16_col(lane)] = cv;
-    if (wave < 8 && l15 < 4) redq[wave * 64 + fdt * 16 + 4 * g + l15] = own;
-    __syncthreads();
-    for (int i = tid; i < 3 * 64; i += NTHR) {
-      const int t = i >> 6, d = i & 63;
-      float sum = 0.f;
-      if (t == 0) {
-#pragma unroll
-        for (int w = 0; w < 8; ++w) sum += redq[w * 64 + d];
-      } else {
-#pragma unroll
-        for (int w = 0; w < NT; ++w) sum += red[(t * NT + w) * 64 + d];
-      }
-      bias_part[(int64_t)b * 3 * D + t * D + h * 64 + d] = sum;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // f32 forward on v_mfma_f32_16x16x4_f32 (CLIP-HBA at the reference's fp32 precision, NEWP:274;
 // config C3): one workgroup (8 waves) per (b, h), K and V of the head in LDS as f32 (<= 2 x 72 KiB,
 // N <= 288), wave = query tile of 16.  Products are exact f32 (the MFMA's f32 form), accumulation f32.
@@ -1742,18 +1480,10 @@ static int bwd_f32mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int
   return 0;
 }
 // VIT_ATTN_BWD_SPLIT=1 keeps the two-kernel backward for every N (A/B runs)
-// bf16 backward form for N <= 224 (vit_sdpa_bwd_variant / VIT_ATTN_BWD_BAND=1 / VIT_ATTN_BWD_SPLIT=1, A/B):
-// 0 = banded where 8 <= NT (N > 112), else whole-head fused; 1 = whole-head fused (the default: the
-// banded form measured 0.276 vs 0.248 ms standalone and -0.8 % in the step, profiles/r04/ab_attn_bwd_band.txt);
-// 2 = the two kernels
+// bf16 backward form for N <= 224 (vit_sdpa_bwd_variant / VIT_ATTN_BWD_SPLIT=1, A/B): 1 = whole-head fused
+// (the default), 2 = the two kernels.  (Round 4's banded-query form measured 0.276 vs 0.248 ms standalone
+// and -0.8 % in the step, profiles/r04/ab_attn_bwd_band.txt, and was removed in round 5.)
 static int g_bwd_variant = -1;
-static bool attn_bwd_band_on() {
-  if (g_bwd_variant < 0) {
-    const char* e = getenv("VIT_ATTN_BWD_BAND");
-    g_bwd_variant = (e && *e == '1') ? 0 : 1;
-  }
-  return g_bwd_variant == 0;
-}
 static bool attn_bwd_split() {
   if (g_bwd_variant == 2) return true;
   static const int v = [] { const char* e = getenv("VIT_ATTN_BWD_SPLIT"); return e && *e == '1' ? 1 : 0; }();
@@ -1764,29 +1494,6 @@ template <int NT>
 static int bwd_mfma(const void* qkv, int64_t ld_qkv, int D, int B, int H, int N, float scale, int causal, const void* o,
                     int64_t ld_o, const void* dout, int64_t ld_do, const float* lse, float* delta,
                     void* dqkv, int64_t ld_dqkv, float* bias_part, hipStream_t s) {
-  if constexpr (NT >= 8 && NT <= 14) {
-    if (!attn_bwd_split() && attn_bwd_band_on() && !g_attn_stamps) {
-      static bool battr = false;
-      if (!battr) {
-        (void)hipFuncSetAttribute((const void*)attn_bwd_band<NT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  BwdB<NT>::LDS);
-        (void)hipFuncSetAttribute((const void*)attn_bwd_band<NT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  BwdB<NT>::LDS);
-        battr = true;
-      }
-#define BWD_BAND(C)                                                                                            \
-  hipLaunchKernelGGL((attn_bwd_band<NT, C>), dim3(B * H), dim3(BwdB<NT>::THREADS), BwdB<NT>::LDS, s,           \
-                     (const bf16*)qkv, ld_qkv, D, H, N, scale, (const bf16*)o, ld_o, (const bf16*)dout, ld_do, lse, \
-                     delta, (bf16*)dqkv, ld_dqkv, bias_part)
-      if (causal)
-        BWD_BAND(true);
-      else
-        BWD_BAND(false);
-#undef BWD_BAND
-      VIT_CHECK_LAUNCH();
-      return 0;
-    }
-  }
   if constexpr (NT <= 14) {
     if (!attn_bwd_split()) {
       static bool attr = false;
@@ -1834,9 +1541,10 @@ int vit_debug_attn_stamps(void* buf) {
   return 0;
 }
 
-// Tuning hook: the bf16 backward form (-1 = from the environment, 0 = banded, 1 = whole-head fused (the
-// default), 2 = two kernels); every form gives the same dq / dk / dv bits.
+// Tuning hook: the bf16 backward form (-1 = from the environment, 1 = whole-head fused (the default),
+// 2 = two kernels); both give the same dq / dk / dv bits.  0 (round 4's banded form) is gone.
 int vit_sdpa_bwd_variant(int v) {
+  if (v == 0 || v > 2) return (int)hipErrorInvalidValue;
   g_bwd_variant = v < 0 ? -1 : v;
   return 0;
 }

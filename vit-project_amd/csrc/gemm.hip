@@ -1142,7 +1142,6 @@ using V6 = Cfg<256, 128, 32, 2, 2, 3, false, 2, 1>;
 using V7 = Cfg<128, 256, 32, 2, 2, 3, false, 2, 1>;  // 4 waves of 64x128
 }  // namespace big
 
-#include "pgemm.inc"
 #include "gemm_f32.inc"
 #include "gemm_w4.inc"
 
@@ -1309,28 +1308,21 @@ static int env_variant(const char* name) {
 }
 
 // per-shape choice among the kept configurations (sweep on MI355X, bs=256 ViT-B/16 shapes)
-static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool pers_ok, bool act_bwd,
-                        bool act_fwd = false) {
+static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool act_bwd) {
   static const int o_fwd = env_variant("VIT_GEMM_FWD"), o_dgrad = env_variant("VIT_GEMM_DGRAD"),
-                   o_wgrad = env_variant("VIT_GEMM_WGRAD"), o_fwd_small = env_variant("VIT_GEMM_FWD_SMALL"),
-                   o_fwd_gelu = env_variant("VIT_GEMM_FWD_GELU"), o_dgrad_small = env_variant("VIT_GEMM_DGRAD_SMALL"),
-                   o_dgrad_gelu = env_variant("VIT_GEMM_DGRAD_GELU");
+                   o_wgrad = env_variant("VIT_GEMM_WGRAD");
   const bool wgrad = split > 1 || (pl == LAY_CR && ql == LAY_CR), fwd = pl == LAY_RC && ql == LAY_RC;
   const int o = wgrad ? o_wgrad : fwd ? o_fwd : o_dgrad;
   int v;
   if (g_variant >= 0) v = g_variant % 100;
   else if (o >= 0) v = o;
   else if (wgrad) v = 11;  // wgrad: 4 waves of 128x128 (w4, round 5; 8 = the round-1..4 ping-pong kernel)
-  else if (fwd && act_fwd && o_fwd_gelu >= 0) v = o_fwd_gelu;               // forward with the GELU pair
-  else if (fwd) v = (N >= 1536 || R >= 1536) ? 5 : (o_fwd_small >= 0 ? o_fwd_small : 5);  // forward
-  // (the N, R < 1536 forwards -- proj, patch embedding -- moved from V2 to V5 in round 3: +0.35 % step,
-  // same-box pairs, bit-identical loss trajectory; VIT_GEMM_FWD_SMALL=2 restores V2)
-  else if (act_bwd && o_dgrad_gelu >= 0) v = o_dgrad_gelu;                // per-shape A/B overrides of the
-  else if (!act_bwd && N <= 1024 && R <= 1024 && o_dgrad_small >= 0) v = o_dgrad_small;  // dgrad rule below
-  else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;                // dgrad (GELU' epilogue: V1, 2 WG/CU)
+  else if (fwd) v = 5;     // forward: V5 (the N, R < 1536 proj / patch embedding too: +0.35 % over V2, round 3)
+  else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;  // dgrad (GELU' epilogue: V1, 2 WG/CU)
+  // (round 5 removed the per-shape overrides VIT_GEMM_{FWD,DGRAD}_{SMALL,GELU}: every re-check measured
+  // their other tiles slower or equal, profiles/r04/ab_dgrad_per_shape.txt, ab_dgrad_gelu_tiles_recheck.txt)
   (void)M;
-  if ((v == 2 || v == 5 || v == 10) && R % 64) v = 1;                       // BK = 64 configurations need 64-row chunks
-  if (v == 10 && (!pers_ok || split > 1)) v = 1;
+  if ((v == 2 || v == 5) && R % 64) v = 1;                                 // BK = 64 configurations need 64-row chunks
   return v;
 }
 
@@ -1413,27 +1405,6 @@ static int num_cus() {
   }
   return n;
 }
-static unsigned g_pers_slot = 0;  // scheduler-counter slot of the next persistent launch (round robin)
-
-template <int PL, int QL, int EPI, typename TO, typename TA>
-static int launch_pers(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, const Epi& e,
-                       hipStream_t s) {
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute((const void*)pers::gemm_kernel<PL, QL, EPI, TO, TA>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, pers::C::LDS);
-    attr = true;
-  }
-  if (R % pers::C::BK) return (int)hipErrorInvalidValue;
-  const int tiles = ((M + pers::C::BM - 1) / pers::C::BM) * ((N + pers::C::BN - 1) / pers::C::BN);
-  const int grid = tiles < num_cus() ? tiles : num_cus();
-  const int slot = (int)(g_pers_slot++ % pers::NSLOT);
-  hipLaunchKernelGGL((pers::gemm_kernel<PL, QL, EPI, TO, TA>), dim3(grid), dim3(pers::C::THREADS), pers::C::LDS, s,
-                     (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, e, slot);
-  VIT_CHECK_LAUNCH();
-  return 0;
-}
-
 // row-tile band of the tile walk per class (tile_coords); VIT_GEMM_GROUP_{FWD,DGRAD}=<row tiles> (A/B)
 // Bands of 8 row tiles help the wide-output GEMMs whose weight operand does not fit beside the
 // row blocks in an XCD's 4 MiB L2 (the fc1 forward GELU pair and the fc2 GELU' input gradient:
@@ -1454,16 +1425,7 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
                        int split, const Epi& e0, hipStream_t s) {
   Epi e = e0;
   if (split <= 1) e.group_m = group_for(PL, QL, N, R);
-  constexpr bool pers_ok = PL == LAY_RC && (EPI == EPI_STORE || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU ||
-                                            EPI == EPI_RESID || EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
-  const int v = pick_variant(PL, QL, M, N, R, split, pers_ok, EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD,
-                             EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_QGELU);
-  if constexpr (pers_ok) {
-    // the persistent kernel's buffer-descriptor stores need full column tiles and 32-bit offsets
-    if (v == 10 && N % pers::C::BN == 0 && (int64_t)M * e.ldc * (int64_t)sizeof(TO) < ((int64_t)1 << 31))
-      return launch_pers<PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, e, s);
-    if (v == 10) return launch_big<big::V1, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
-  }
+  const int v = pick_variant(PL, QL, M, N, R, split, EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
   if constexpr (PL == LAY_CR && QL == LAY_CR) {  // w4 ring / load-placement A/B (tools/bench_kernels.py --sweep)
     if (v == 12) return launch_w4<w4::Cfg<4, 0>, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     if (v == 13) return launch_w4<w4::Cfg<4, 2>, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
@@ -1490,7 +1452,6 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
 struct SkWs { int dev; hipStream_t s; float* part; int64_t part_bytes; int* cnt; int ncnt; };
 static SkWs g_sk[32];
 static int g_nsk = 0;
-static int g_sk_mode = -2;  // VIT_GEMM_STREAMK: 0 off, 1 on (default: on where it removes a ragged round), 2 all k-steps shared
 static int stream_device(hipStream_t s) {  // the null stream: the current device
   hipDevice_t d = -1;
   return hipStreamGetDevice(s, &d) == hipSuccess ? (int)d : -1;
@@ -1518,18 +1479,15 @@ static int launch_f32(const void* P, int64_t ldp, const void* Q, int64_t ldq, in
                               hipFuncAttributeMaxDynamicSharedMemorySize, f32m::LDS + 16);
     attr = true;
   }
-  if (g_sk_mode == -2) {
-    const char* v = getenv("VIT_GEMM_STREAMK");
-    g_sk_mode = v ? atoi(v) : 1;
-  }
   const int64_t tiles = (int64_t)((M + f32m::BM - 1) / f32m::BM) * ((N + f32m::BN - 1) / f32m::BN);
   const int G = 2 * num_cus();  // two workgroups per CU
-  if (split <= 1 && g_sk_mode >= 1 && R % f32m::BK == 0 && tiles >= G && ragged_waste(tiles, G) > 0.03) {
+  if (split <= 1 && R % f32m::BK == 0 && tiles >= G && ragged_waste(tiles, G) > 0.03) {
     const SkWs* w = sk_for(s);
     if (w && w->ncnt >= G && w->part_bytes >= (int64_t)G * 2 * f32m::BM * f32m::BN * 4) {
-      // tile-aligned rounds, then the last full round plus the remainder shared by k-steps
-      // (VIT_GEMM_STREAMK=2: every tile shared by k-steps)
-      const int dp_rounds = g_sk_mode == 2 ? 0 : (int)(tiles / G) - 1;
+      // tile-aligned rounds, then the last full round plus the remainder shared by k-steps (sharing every
+      // tile by k-steps from the start was 2-7 % slower on the tall forwards, round 3; that form and the
+      // VIT_GEMM_STREAMK A/B switch were removed in round 5)
+      const int dp_rounds = (int)(tiles / G) - 1;
       hipLaunchKernelGGL((f32m::gemm_sk_kernel<PL, QL, EPI, TO, float>), dim3(G), dim3(f32m::THREADS),
                          f32m::LDS + 16, s, (const float*)P, ldp, (const float*)Q, ldq, M, N, R, dp_rounds, e,
                          w->part, w->cnt);
@@ -1734,52 +1692,12 @@ int vit_gemm_splitk(int p_layout, int q_layout, int M, int N, int R, const float
   return 0;
 }
 
-// The multi-tile deferred-store kernel (gemm_ms.hip) for the bf16 forwards (plain / GELU pair) and the
-// plain bf16 input gradients: VIT_GEMM_MS = bit mask (1 = forwards, 2 = input gradients; 0 = off, A/B),
-// VIT_GEMM_MS_CFG = its configuration (vit_gemm_ms cfg: row tile and store deferral), VIT_GEMM_MS_T =
-// tiles per workgroup (the grid is ceil(tiles / T)); a forced tile variant (vit_gemm_variant, the
-// tuning sweeps) bypasses it.
-extern "C" int vit_gemm_ms(int epi, int wl, int bm, int M, int N, int K, const void* X, int64_t ldx, const void* W,
-                           int64_t ldw, const float* bias, void* C, int64_t ldc, void* C2, int grid, void* stream);
-static int g_ms[3] = {-2, 0, 2};  // class mask, cfg, tiles per workgroup; -2 = not yet read from the environment
-static bool ms_on(int wl) {
-  if (g_ms[0] == -2) {
-    const int on = env_variant("VIT_GEMM_MS"), cfg = env_variant("VIT_GEMM_MS_CFG"), t = env_variant("VIT_GEMM_MS_T");
-    g_ms[0] = on == -1 ? 0 : on;
-    if (cfg >= 0) g_ms[1] = cfg;
-    if (t >= 1) g_ms[2] = t;
-  }
-  return (g_ms[0] >> wl & 1) && g_variant < 0;
-}
-// hipErrorInvalidValue from vit_gemm_ms = shape outside its contract: the caller takes the V* kernels
-static int try_ms(int epi, int wl, int M, int N, int K, const void* X, int64_t ldx, const void* W, int64_t ldw,
-                  const float* bias, void* C, int64_t ldc, void* C2, hipStream_t s) {
-  if (!ms_on(wl)) return (int)hipErrorInvalidValue;
-  const int bm = (g_ms[1] == 1 || g_ms[1] == 2) ? 256 : 192;
-  const int tiles = ((M + bm - 1) / bm) * (N / 256);
-  const int grid = (tiles + g_ms[2] - 1) / g_ms[2];
-  return vit_gemm_ms(epi, wl, g_ms[1], M, N, K, X, ldx, W, ldw, bias, C, ldc, C2, grid, s);
-}
-
-// Tuning hook (A/B runs): the multi-tile kernel's class mask (1 forwards, 2 input gradients), its row tile
-// and tiles per workgroup (-1 keeps one).
-int vit_gemm_ms_config(int on, int cfg, int tiles_per_wg) {
-  (void)ms_on(0);
-  if (on >= 0) g_ms[0] = on;
-  if (cfg >= 0) g_ms[1] = cfg;
-  if (tiles_per_wg >= 1) g_ms[2] = tiles_per_wg;
-  return 0;
-}
-
 // F.linear forward: Y[M,N] = X[M,K] W[N,K]^T + b with a fused epilogue
 //   epi = EPI_STORE (Y out_dtype), EPI_BIAS_GELU / EPI_BIAS_QGELU (Y = act'(pre), act_out = act(pre)),
 //   EPI_RESID (Y f32 = resid + X W^T + b; Y may alias resid).
 int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const void* X, int64_t ldx,
                    const void* W, const float* bias, void* Y, int64_t ldy, const void* resid,
                    void* act_out, void* stream) {
-  if (dtype == VIT_BF16 && out_dtype == VIT_BF16 && (epi == EPI_STORE || epi == EPI_BIAS_GELU) &&
-      try_ms(epi == EPI_BIAS_GELU, 0, M, N, K, X, ldx, W, K, bias, Y, ldy, act_out, (hipStream_t)stream) == 0)
-    return 0;
   Epi e = make_epi();
   e.C = Y; e.ldc = ldy; e.bias = bias; e.aux = resid; e.ld_aux = ldy; e.aux_out = act_out;
   return gemm_any(epi, dtype, out_dtype, LAY_RC, LAY_RC, M, N, K, X, ldx, W, K, 1, e, (hipStream_t)stream);
@@ -1799,9 +1717,6 @@ int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, con
                      const void* W, void* dX, int64_t lddx, const void* pre, float* dbias, float* partial,
                      int64_t partial_floats, int defer_reduce, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VIT_BF16 && out_dtype == VIT_BF16 && epi == EPI_STORE && !dbias &&
-      try_ms(0, 1, M, K, N, dY, lddy, W, K, nullptr, dX, lddx, nullptr, s) == 0)
-    return 0;
   Epi e = make_epi();
   e.C = dX; e.ldc = lddx; e.aux = pre; e.ld_aux = lddx;
   const int rows = (M + 63) / 64;
@@ -1959,7 +1874,7 @@ int vit_linear_wgrad_partials2(int M, int split, int Na, int Ka, const void* dYa
   };
   const big::PPProb a = prob(dYa, lddya, Xa, ldxa, Na, Ka, slabs_a), b = prob(dYb, lddyb, Xb, ldxb, Nb, Kb, slabs_b);
   // the weight-gradient kernel pick_variant chooses (11 = w4, 8 = the ping-pong kernel; VIT_GEMM_WGRAD A/B)
-  if (pick_variant(LAY_CR, LAY_CR, Na, Ka, M, split, false, false) == 8) {
+  if (pick_variant(LAY_CR, LAY_CR, Na, Ka, M, split, false) == 8) {
     using C = big::PP<4>;
     static bool attr = false;
     if (!attr) {

@@ -27,8 +27,6 @@ SIGNATURES = {
     "vit_abi_version": [],
     "vit_gemm_variant": [i32],
     "vit_gemm_group": [i32, i32],
-    "vit_gemm_ms": [i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, vp, i64, vp, i32, vp],
-    "vit_gemm_ms_config": [i32, i32, i32],
     "vit_gemm_streamk_workspace": [vp, vp, i64, vp, i32],
     "vit_gemm_rc_chunk_rows": [i32, i64],
     "vit_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, vp],

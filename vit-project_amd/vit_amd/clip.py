@@ -36,7 +36,6 @@ is bit-identical to recomputing it.
 from __future__ import annotations
 
 import math
-import os
 from collections import OrderedDict
 
 import torch
@@ -45,13 +44,11 @@ import torch.nn as nn
 from . import _lib as L
 from . import ops
 from .dora import DoRALayer
-from .model import _FUSED_RESID, _FUSED_RESID_F32, _BlockFn, _Shadowed, _gout, _wt
+from .model import _FUSED_RESID_F32, _BlockFn, _Shadowed, _gout, _wt
 
 SOT, EOT = 49406, 49407
 
 
-# VIT_CLIP_PATCH_PAD=0: the unpadded 588-column patch embedding (scalar-FMA GEMM) -- A/B only
-_PATCH_PAD = [os.environ.get("VIT_CLIP_PATCH_PAD", "1") != "0"]
 
 
 def _padded_weight(mod, w2, Kp):
@@ -338,7 +335,7 @@ class CLIP(nn.Module):
         # ViT-L/14's 3*14*14 = 588 patch columns are padded to a multiple of the GEMM's 32-deep k-step
         # (zeros in U and in the weight), so the patch embedding runs on the MFMA path
         K = v.conv1.in_channels * ps * ps
-        Kp = -(-K // 32) * 32 if _PATCH_PAD[0] else K
+        Kp = -(-K // 32) * 32
         U = ops.patch_unfold(image.to(torch.float32).contiguous(), ps, T, ld=Kp)
         npatch = U.shape[0] // B
         pos = v.positional_embedding.detach()
@@ -356,7 +353,7 @@ class CLIP(nn.Module):
         first = _first_trainable(blocks)
         # the residual adds run inside the next LayerNorm (as the ViT blocks, model._tokens); in f32 the
         # same f32 add as the GEMM's residual epilogue, so the reference-precision result is unchanged
-        rs = ({"pending": None} if (_FUSED_RESID[0] and (T != torch.float32 or _FUSED_RESID_F32[0]) and ops.add_layer_norm_supported(W))
+        rs = ({"pending": None} if ((T != torch.float32 or _FUSED_RESID_F32[0]) and ops.add_layer_norm_supported(W))
               else None)
         for i, blk in enumerate(blocks):
             cfg = self._cfg(heads, False, frozen=i < first)

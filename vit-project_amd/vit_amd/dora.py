@@ -13,7 +13,6 @@ reads ``.weight``: quirk Q5, but part of the class's surface).
 from __future__ import annotations
 
 import math
-import os
 
 import torch
 import torch.nn as nn
@@ -23,8 +22,6 @@ from . import ops
 from ._lib import call, ptr
 
 
-# VIT_DORA_SPLITK=0: the factor-gradient GEMMs unsplit (24-32 workgroups each) -- A/B only
-_SPLITK = [os.environ.get("VIT_DORA_SPLITK", "1") != "0"]
 
 class _DoraWeightFn(torch.autograd.Function):
     @staticmethod
@@ -55,7 +52,7 @@ class _DoraWeightFn(torch.autograd.Function):
         dA = torch.empty_like(A)
         dB = torch.empty_like(Bm)
         # sdDnT [out, in] f32, then the split-K slabs of the two factor GEMMs (16-B aligned)
-        slab_floats = 2 * 256 * 1024 if _SPLITK[0] else 0
+        slab_floats = 2 * 256 * 1024
         base = -(-fout * fin // 4) * 4
         ws = ops.workspace("dora_sdDnT", (base + slab_floats) * 4, dev).view(torch.float32)
         call("vit_dora_weight_bwd_ws", fin, fout, r, ptr(m), ptr(A), ptr(Bm), ptr(gW), ptr(DnT), float(ctx.scaling),

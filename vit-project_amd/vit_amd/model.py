@@ -67,8 +67,6 @@ _OVERLAP = [True]
 # forward half-batch chains: join the two streams after every block ("block") or once after
 # the block stack ("end", default)
 _FWD_JOIN = [os.environ.get("VIT_FWD_JOIN", "end")]
-# VIT_FWD_SPLIT=0: the forward as one full-batch chain on the caller's stream (A/B runs)
-_FWD_SPLIT = [os.environ.get("VIT_FWD_SPLIT", "1") != "0"]
 # block backward: join the side stream (weight/bias gradients) at the end of every block
 # ("block") or once, in the patch embedding's backward ("end": flat-gradient runs only)
 _BWD_JOIN = [os.environ.get("VIT_BWD_JOIN", "end")]
@@ -78,30 +76,13 @@ _HOLD_REFS = [os.environ.get("VIT_HOLD_REFS", "1") != "0"]
 # ~0.3 ms later (bs=256).  Default B/32 (8 at bs=256): +0.8 %; 16+ falls off a GEMM tile-count
 # cliff (-3 %).  profiles/r01/ab_fwd_half_split.json
 _FWD_HALF_DELTA = [None if os.environ.get("VIT_FWD_HALF_DELTA") is None else int(os.environ["VIT_FWD_HALF_DELTA"])]
-# forward: launches of each block the caller's chain queues before the side chain is released
-_FWD_STAGGER = [int(os.environ.get("VIT_FWD_STAGGER", "0"))]
 _HOLD = {}
 
 
-# VIT_FUSED_RESID=0: the proj / fc2 GEMMs add into the f32 residual stream in their epilogue
-# (EPI_RESID) instead of the following LayerNorm doing it (A/B runs)
-_FUSED_RESID = [os.environ.get("VIT_FUSED_RESID", "1") != "0"]
-# ... and in fp32 compute with VIT_FUSED_RESID_F32=1 (bit-identical: the same f32 add, in the LayerNorm
-# instead of the epilogue; C3 fp32 measured 607 vs 609 img/s, so the f32 GEMM epilogue keeps it by default)
+# bf16: the proj / fc2 outputs are added into the f32 residual stream by the following LayerNorm
+# (+2.0 % over the EPI_RESID epilogue, round 2); fp32 keeps the epilogue add unless VIT_FUSED_RESID_F32=1
+# (bit-identical: the same f32 add, in the LayerNorm; C3 fp32 measured 607 vs 609 img/s)
 _FUSED_RESID_F32 = [os.environ.get("VIT_FUSED_RESID_F32", "0") == "1"]
-# VIT_COL_BATCH=0: every bias / LayerNorm-affine reduction of a block's backward as its own launch(es)
-# (the round-2 schedule: ~9 launches per block) instead of one vit_colreduce_batch launch per block
-_COL_BATCH = [os.environ.get("VIT_COL_BATCH", "1") != "0"]
-# VIT_WGRAD_PAIRS: 1 (default) = fc2 + fc1 and proj + qkv weight gradients as one grouped launch each;
-# 0 = each as its own launch (with COL_BATCH; fc2's and proj's then start before their block's input-
-# gradient kernels, as soon as their operands exist); 2 = only the MLP pair grouped; 3 = only the
-# attention pair grouped
-_WGRAD_PAIRS = [os.environ.get("VIT_WGRAD_PAIRS", "1")]
-
-
-def _pair_on(which: str) -> bool:
-    v = _WGRAD_PAIRS[0]
-    return v == "1" or (v == "2" and which == "mlp") or (v == "3" and which == "attn")
 
 
 def set_wgrad_overlap(enable: bool):
@@ -109,29 +90,9 @@ def set_wgrad_overlap(enable: bool):
     _OVERLAP[0] = bool(enable)
 
 
-# VIT_SIDE_CUS=k (A/B only): the side stream restricted to k of the 256 CUs by a HIP CU mask
-# (hipExtStreamCreateWithCUMask; k spread evenly over the mask bits), instead of dynamic sharing
-_SIDE_CUS = [int(os.environ.get("VIT_SIDE_CUS", "0"))]
-
-
-def _side_stream(dev):
-    k = _SIDE_CUS[0]
-    if k <= 0:
-        return torch.cuda.Stream(device=dev)
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
-    bits = [(i * k) // ncu != ((i + 1) * k) // ncu for i in range(ncu)]  # k of ncu, evenly spread
-    words = (ctypes.c_uint32 * ((ncu + 31) // 32))()
-    for i, on in enumerate(bits):
-        if on:
-            words[i // 32] |= 1 << (i % 32)
-    handle = ctypes.c_void_p()
-    with torch.cuda.device(dev):
-        rc = hip.hipExtStreamCreateWithCUMask(ctypes.byref(handle), ctypes.c_uint32(len(words)), words)
-    if rc != 0:
-        raise RuntimeError(f"hipExtStreamCreateWithCUMask failed ({rc})")
-    return torch.cuda.ExternalStream(handle.value, device=dev)
+# (round 5 removed the A/B switches whose other settings all measured slower or equal: VIT_FWD_STAGGER,
+# VIT_WGRAD_PAIRS, VIT_SIDE_CUS -- records in profiles/r04/ab_fwd_stagger_recheck.txt,
+# ab_wgrad_pairing_recheck.txt and DESIGN.md §4.6)
 
 
 def fwd_split(B: int) -> int:
@@ -148,7 +109,7 @@ class _Side:
         self.on = _OVERLAP[0] and dev.type == "cuda"
         if self.on:
             if dev not in _SIDE:
-                _SIDE[dev] = _side_stream(dev)
+                _SIDE[dev] = torch.cuda.Stream(device=dev)
             self.side = _SIDE[dev]
 
     def run(self, fn):
@@ -391,19 +352,16 @@ class _BlockFn(torch.autograd.Function):
                 f()
 
         side = _Side(dev)
-        if side.on and B >= 2 and T != torch.float32 and _FWD_SPLIT[0]:
+        if side.on and B >= 2 and T != torch.float32:
             # two half-batch chains on two streams: one chain's GEMM epilogues (HBM-bound)
-            # overlap the other's MFMA main loops.  The side chain is released (side.run waits for
-            # everything the caller's stream has queued) after the caller's first _FWD_STAGGER
-            # launches of this block, so the two chains run out of phase by that many kernels.
+            # overlap the other's MFMA main loops (side.run waits for everything the caller's stream
+            # has queued, so the side chain starts with the caller's)
             hb = fwd_split(B)
             mine, other = chain(0, hb), chain(hb, B)
-            k = max(0, min(len(mine), _FWD_STAGGER[0]))
-            run(mine[:k])
             side.run(lambda: run(other))
             side.guard(x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act, xo,
                        *(t for t in (pb, yb, *(pend or ())) if t is not None))
-            run(mine[k:])
+            run(mine)
             # each half only feeds the same half of the next block: a stack of blocks joins
             # once after its last block (cfg "defer_join", ViT._tokens) instead of per block
             if not cfg.get("defer_join"):
@@ -452,19 +410,17 @@ class _BlockFn(torch.autograd.Function):
         # gradient: fc2.bias from the upstream LayerNorm backward (side channel), fc1.bias
         # from the GELU' dgrad epilogue, proj.bias from LN2 backward, qkv.bias from SDPA backward.
         # every deferred column reduction of this block goes into ONE launch at its end (side stream)
-        rb = ops.ColBatch() if _COL_BATCH[0] else side
-        rbw = rb if _COL_BATCH[0] else None  # the weight gradients' split-K slab sums join the same launch
+        # every bias / LayerNorm-affine reduction and the weight gradients' split-K slab sums of this block
+        # in one batched launch (vit_colreduce_batch) on the side stream
+        rb = rbw = ops.ColBatch()
         if ng[12]:
             if dxo_sum is not None:  # the upstream LayerNorm backward's column sums (side stream)
-                if _COL_BATCH[0]:
-                    rb.add(dxo_sum.view(1, D), 1, D, g[12])
-                else:
-                    side.run(lambda: ops.colreduce(dxo_sum, 1, D, g[12]))
+                rb.add(dxo_sum.view(1, D), 1, D, g[12])
             else:
                 ops.colsum(dxo_c, out=g[12])
         # weight gradients in pairs over the same token rows (fc2 + fc1, proj + qkv): one grouped
-        # launch each, half the split-K slabs of two launches (VIT_WGRAD_PAIRS=0: one launch each)
-        pair_mlp = rbw is not None and _pair_on("mlp") and ng[11] and ng[9] and need_mlp_in
+        # launch each, half the split-K slabs of two launches
+        pair_mlp = rbw is not None and ng[11] and ng[9] and need_mlp_in
         if ng[11] and not pair_mlp:
             side.run(lambda: ops.linear_wgrad(dxo_c, act, out=g[11], reduce_on=rbw))
         dx = None
@@ -484,13 +440,13 @@ class _BlockFn(torch.autograd.Function):
             # attention
             # block 0 (the patch rows' block, last in the backward): its last weight gradients are the tail
             tail = bool(compact_np)
-            pair_attn = rbw is not None and _pair_on("attn") and ng[5] and ng[3] and need_attn
+            pair_attn = rbw is not None and ng[5] and ng[3] and need_attn
             if ng[5] and not pair_attn:
                 side.run(lambda: ops.linear_wgrad(dxm_c, o, out=g[5], tail=tail, reduce_on=rbw))
             if need_attn:
                 do = ops.linear_dgrad(dxm_c, Wproj, out_dtype=T)
                 dqkv = ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dbias=g[4], causal=causal,
-                                    reduce_on=rb if _COL_BATCH[0] else None)
+                                    reduce_on=rb)
                 if pair_attn:
                     side.run(lambda: ops.linear_wgrad_pair((dxm_c, o, g[5]), (dqkv, h1, g[3]), rbw, tail=tail))
                 elif ng[3]:
@@ -509,9 +465,8 @@ class _BlockFn(torch.autograd.Function):
                                    reduce_on=rb)
                 if ng[0] and (dx_c is not None or dsum is not None):
                     _put_copy(dx, dx_c, dsum)
-        if _COL_BATCH[0]:
-            side.run(rb.launch)
-            side.guard(*rb.parts)
+        side.run(rb.launch)
+        side.guard(*rb.parts)
         side.guard(dxo, dxo_c, dxo_sum, x2, h1, m1, r1, qkv, o, lse, xm, h2, m2, r2, dact, act,
                    *(v for v in (dpre, dxm, dxm_c, do, dqkv, dx) if v is not None))
         if cfg_defer_bwd(ctx):
@@ -761,7 +716,7 @@ class VisionTransformer(nn.Module):
         # fp8 attention (set_attention_fp8): forward passes that build no graph (eval / RSA)
         cfg["attn_fp8"] = self._attn_fp8 and not torch.is_grad_enabled()
         D = self.embed_dim
-        if _FUSED_RESID[0] and (self.compute_dtype != torch.float32 or _FUSED_RESID_F32[0]) and ops.add_layer_norm_supported(D):
+        if (self.compute_dtype != torch.float32 or _FUSED_RESID_F32[0]) and ops.add_layer_norm_supported(D):
             cfg["resid"] = {"pending": None}  # residual adds inside the LayerNorms (_BlockFn.forward)
         for i, blk in enumerate(self.blocks):
             bcfg = cfg if i != 0 else dict(cfg, compact_np=pe.num_patches)

@@ -338,9 +338,6 @@ def add_layer_norm_fwd(x2d, r2d, xs, w=None, b=None, eps=1e-6, out=None, mean=No
     return xs
 
 
-_LN_MULTI = [os.environ.get("VIT_LN_MULTI", "1") != "0"]
-
-
 def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0, dx_copy=None, ld_copy=0,
                    compact_np=0, dgamma=None, dbeta=None, dsum=None, ws="ln_partial", reduce_on=None):
     """dsum [D] (optional) receives the column sums of dx (a Linear bias gradient).
@@ -371,11 +368,7 @@ def layer_norm_bwd(x, ldx, dy, w, mean, rstd, dx, lddx, rows, dres=None, ldres=0
         def finish():
             _keep(part)
             # the [dgamma | dbeta | dsum] partials are stacked: one launch per reduction stage
-            if not _LN_MULTI[0]:
-                for q, o in enumerate((dgamma, dbeta, dsum)):
-                    if o is not None:
-                        colreduce(part[q * nb * D:(q + 1) * nb * D], nb, D, o, scratch=sc)
-            elif dgamma is not None:
+            if dgamma is not None:
                 call("vit_colreduce_multi", ptr(part), 3 if dsum is not None else 2, nb, D, ptr(dgamma),
                      ptr(dbeta), ptr(dsum), 0, ptr(sc), _s(dgamma))
             else:
@@ -554,15 +547,12 @@ def mse_bwd(pred, target, grad_loss=None):
     return d
 
 
-# VIT_GEMM_SPLITK_SMALL=0: small f32 GEMMs (CLIP-HBA's pooled head / logits, < 128 tiles of 32 x 32 over
-# reductions >= 256) unsplit on the generic kernel -- A/B only
-_SPLITK_SMALL = [os.environ.get("VIT_GEMM_SPLITK_SMALL", "1") != "0"]
 
 
 def gemm(P, p_layout, Q, q_layout, M, N, R, out=None, out_dtype=torch.float32, bias=None):
     """Raw C[i][j] = sum_r P(i,r) Q(j,r) (+bias[j]); layouts L.LAY_RC (r contiguous) / L.LAY_CR."""
     assert P.dtype == Q.dtype and P.stride(-1) == 1 and Q.stride(-1) == 1
-    if (_SPLITK_SMALL[0] and out is None and bias is None and P.dtype == torch.float32 and out_dtype == torch.float32
+    if (out is None and bias is None and P.dtype == torch.float32 and out_dtype == torch.float32
             and R >= 256 and ((M + 31) // 32) * ((N + 31) // 32) < 128):
         # few output tiles over a long reduction: split it (vit_gemm_splitk, slab sum in a fixed order)
         out = torch.empty(M, N, dtype=torch.float32, device=P.device)
