@@ -11,6 +11,7 @@
 #               WRITE_SIZE -> pmc_step_classes.json (MFMA busy, HBM GB/s per kernel)
 #   kernels     tools/bench_kernels.py (standalone kernel table)
 #   c3          tools/bench_clip.py (config C3 leg alone)
+#   wgrad       tools/bench_wgrad.py (weight-gradient kernels / pairs per variant)
 set -o pipefail
 O=gpurun_out/$1
 shift
@@ -54,6 +55,9 @@ for step in "$@"; do
     kernels)
       timeout -k 10 300 python tools/bench_kernels.py $arg > "$O/kernels.jsonl" 2>&1 || fail kernels "$O/kernels.jsonl"
       tail -30 "$O/kernels.jsonl" ;;
+    wgrad)
+      timeout -k 10 300 python -u tools/bench_wgrad.py $arg > "$O/wgrad.jsonl" 2>&1 || fail wgrad "$O/wgrad.jsonl"
+      cat "$O/wgrad.jsonl" ;;
     c3)
       timeout -k 10 400 python -u tools/bench_clip.py $arg > "$O/c3.json" 2> "$O/c3.err" || fail c3 "$O/c3.err"
       cat "$O/c3.json" ;;
