@@ -202,7 +202,7 @@ int vit_sdpa_bwd(int dtype, int B, int H, int N, int head_dim, const void* qkv, 
 int vit_sdpa_bwd_partial_floats(int B, int N, int D);
 /* Tuning hook: the bf16 backward form for N <= 224 (-1 = from VIT_ATTN_BWD_SPLIT, 1 = whole-head fused
  * (the default), 2 = two kernels; 0, round 4's banded form, was removed in ABI 8: hipErrorInvalidValue).
- * Both forms give bit-identical dq / dk / dv. */
+ * The two forms agree to bf16 rounding (some f32 sums are ordered differently). */
 int vit_sdpa_bwd_variant(int v);
 
 /* torch.nn.functional.cross_entropy(outputs, targets) mean (VIT:140) and its gradient. */

@@ -469,6 +469,32 @@ def test_patch_embed_padded_reduction_on_mfma_path():
         _close(x, ref, rel, f"padded patch {dt}")
 
 
+def test_f32_streamk_graph_replay_matches_eager():
+    """an f32 GEMM captured on a stream registered before capture (ops.register_capture_stream)
+    takes the same stream-K form as the eager launch on that stream, so graph replay and eager agree bit
+    for bit (C3's 64 x 257-row shapes: 1032 tiles of 128 x 128 on 512 slots, a ragged last round)."""
+    M, N, K = 64 * 257, 1024, 1024
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = torch.randn(M, K, device=DEV, generator=g)
+    w = torch.randn(N, K, device=DEV, generator=g) * 0.05
+    s = torch.cuda.Stream()
+    ops.register_capture_stream(s)
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        eager = ops.linear_fwd(x, w, None, out_dtype=torch.float32)
+        out = torch.empty_like(eager)
+        ops.linear_fwd(x, w, None, out=out)  # warm-up of the captured call's exact arguments
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        ops.linear_fwd(x, w, None, out=out)
+    out.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, eager)
+    _close(out, (x.double() @ w.double().T).float(), 1e-5, "stream-K replay")
+
+
 @pytest.mark.parametrize("M,N,R", [(64, 66, 768), (32, 1024, 4096), (1024, 32, 1024), (64, 768, 1024)])
 def test_gemm_splitk_matches_reference(M, N, R):
     """vit_gemm_splitk (round 4: DoRA factor gradients, CLIP-HBA head GEMMs): every layout pair against a
@@ -706,8 +732,9 @@ def test_sdpa_bwd_large_grid(B, H, N, causal):
                                       (224, True)])
 def test_sdpa_bwd_fused_matches_two_kernel(N, causal):
     """The whole-head fused backward (the default for N <= 224) against the two-kernel form (dq kernel +
-    dk/dv kernel, the N > 224 path): dq / dk / dv bit-identical (same MFMA order per output), delta
-    identical, the qkv-bias column sums within fp32 summation-order error; B*H = 300 workgroups."""
+    dk/dv kernel, the N > 224 path): dq / dk / dv agree to bf16 rounding (the forms order some f32
+    sums differently: up to one bf16 ulp apart), delta to fp32 rounding, the qkv-bias column sums within
+    2e-4 of scale (summed from differently rounded partials); B*H = 300 workgroups."""
     B, H = 25, 12
     D = H * 64
     g = torch.Generator(device=DEV).manual_seed(37)
@@ -728,9 +755,9 @@ def test_sdpa_bwd_fused_matches_two_kernel(N, causal):
     finally:
         lib.vit_sdpa_bwd_variant(-1)
     (d0, b0, l0), (d1, b1, l1) = outs
-    assert torch.equal(d0, d1), (d0.float() - d1.float()).abs().max().item()
-    assert torch.equal(l0, l1)
-    _close(b1, b0, 1e-5, "qkv bias grad (two-kernel vs fused)")
+    _close(d1, d0, 8e-3, "dqkv (two-kernel vs fused)")
+    _close(l1, l0, 1e-6, "delta")
+    _close(b1, b0, 2e-4, "qkv bias grad (two-kernel vs fused)")
 
 
 @pytest.mark.parametrize("N", [77, 16, 197, 224])

@@ -1542,7 +1542,7 @@ int vit_debug_attn_stamps(void* buf) {
 }
 
 // Tuning hook: the bf16 backward form (-1 = from the environment, 1 = whole-head fused (the default),
-// 2 = two kernels); both give the same dq / dk / dv bits.  0 (round 4's banded form) is gone.
+// 2 = two kernels; they agree to bf16 rounding).  0 (round 4's banded form) is gone.
 int vit_sdpa_bwd_variant(int v) {
   if (v == 0 || v > 2) return (int)hipErrorInvalidValue;
   g_bwd_variant = v < 0 ? -1 : v;

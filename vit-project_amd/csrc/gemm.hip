@@ -1456,10 +1456,15 @@ static int stream_device(hipStream_t s) {  // the null stream: the current devic
   hipDevice_t d = -1;
   return hipStreamGetDevice(s, &d) == hipSuccess ? (int)d : -1;
 }
+// the device query runs only when a registered handle matches (not on every f32 GEMM
+// dispatch; hipStreamGetDevice is a host-side lookup, legal on a capturing stream)
 static const SkWs* sk_for(hipStream_t s) {
-  const int d = stream_device(s);
-  for (int i = 0; i < g_nsk; ++i)
-    if (g_sk[i].s == s && g_sk[i].dev == d) return &g_sk[i];
+  int d = -2;
+  for (int i = 0; i < g_nsk; ++i) {
+    if (g_sk[i].s != s) continue;
+    if (d == -2) d = stream_device(s);
+    if (g_sk[i].dev == d) return &g_sk[i];
+  }
   return nullptr;
 }
 // fraction of the last round's workgroup slots a plain launch of `tiles` leaves empty

@@ -51,12 +51,15 @@ def _keep(t: torch.Tensor):
 _SK = {}  # (device index, stream handle) -> (part, counters) registered with vit_gemm_streamk_workspace
 
 
-def _streamk(device):
+def _streamk(device, stream=None):
     """Register (once per (device, stream)) the stream-K workspace the f32 MFMA GEMMs use on the
-    current stream.  Keyed by device too: the null stream has handle 0 on every device.  Under
-    graph capture an unregistered stream stays unregistered (the workspace's zero-fill would be
-    captured, not run, and its memory would come from the graph's pool): the plain launch runs."""
-    st = L.stream_ptr(device)
+    current stream (or ``stream``).  Keyed by device too: the null stream has handle 0 on every device.
+    Under graph capture an unregistered stream stays unregistered (the workspace's zero-fill would be
+    captured, not run, and its memory would come from the graph's pool): the plain launch runs there.
+    The two forms sum k in different orders, so an f32 GEMM that ran stream-K eagerly and as the plain
+    launch in a replayed graph agree to rounding, not bit for bit -- unless the capture
+    stream was registered before capture: ``register_capture_stream``."""
+    st = L.stream_ptr(device) if stream is None else stream.cuda_stream
     key = (torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device(), st)
     if key in _SK or torch.cuda.is_current_stream_capturing():
         return
@@ -66,6 +69,13 @@ def _streamk(device):
     with torch.cuda.device(key[0]):
         call("vit_gemm_streamk_workspace", st, ptr(part), part.numel() * 4, ptr(cnt), g)
     _SK[key] = (part, cnt)
+
+
+def register_capture_stream(stream, device=None):
+    """Give ``stream`` (e.g. the side stream a ``torch.cuda.graph`` captures on) its stream-K workspace
+    before capture, so the f32 GEMMs captured on it take the same stream-K form -- and the same bits --
+    as the eager launches on a registered stream."""
+    _streamk(stream.device if device is None else device, stream)
 
 
 def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, resid=None, act_out=None):
