@@ -13,6 +13,7 @@
 #   c3          tools/bench_clip.py (config C3 leg alone)
 #   wgrad       tools/bench_wgrad.py (weight-gradient kernels / pairs per variant)
 #   w4b         tools/lab/w4b_lab.py (the two-workgroup-per-CU w4 loop vs the library forward / dgrad)
+#   w4r         tools/lab/w4r_lab.py (register-staged w4 weight gradient vs the LDS-DMA one)
 set -o pipefail
 O=gpurun_out/$1
 shift
@@ -62,6 +63,9 @@ for step in "$@"; do
     w4b)
       timeout -k 10 300 python -u tools/lab/w4b_lab.py $arg > "$O/w4b.jsonl" 2>&1 || fail w4b "$O/w4b.jsonl"
       cat "$O/w4b.jsonl" ;;
+    w4r)
+      timeout -k 10 300 python -u tools/lab/w4r_lab.py $arg > "$O/w4r.jsonl" 2>&1 || fail w4r "$O/w4r.jsonl"
+      cat "$O/w4r.jsonl" ;;
     c3)
       timeout -k 10 400 python -u tools/bench_clip.py $arg > "$O/c3.json" 2> "$O/c3.err" || fail c3 "$O/c3.err"
       cat "$O/c3.json" ;;
