@@ -455,9 +455,9 @@ def main(a):
     mfma_busy, busy_src, busy_sha = _pmc_mfma_busy()
     src_sha = wgrad_src_sha()
     if wg is not None:
-        roof = {"bound": "mfma", "kernel": "w4::kernel2 / w4::kernel (split-K weight-gradient GEMM, 256x256x32 tile "
-                                           "on 4 waves of 128x128, AGPR accumulators; fc2+fc1 and proj+qkv as grouped "
-                                           "pairs): every bf16 dW = dY^T X of the step",
+        roof = {"bound": "mfma", "kernel": "big::pp_kernel2 / pp_kernel (split-K weight-gradient GEMM, 256x256x32 "
+                                           "ping-pong; fc2+fc1 and proj+qkv as grouped pairs; VIT_GEMM_WGRAD=11 selects "
+                                           "the w4 kernel): every bf16 dW = dY^T X of the step",
                 "achieved": wg["tflops"], "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
                 "frac": round(wg["tflops"] / PEAK_BF16_TFLOPS, 4), "traffic": traffic,
                 "measured": "in-step: HIP events around each launch on the side stream it runs on, over the timed "
@@ -478,7 +478,7 @@ def main(a):
                 "counters_src_sha": {"kernel_sources": src_sha, "traffic": traffic_sha, "mfma_busy": busy_sha},
                 "counters_match_kernel": traffic_sha == src_sha and busy_sha == src_sha}
     else:
-        roof = {"bound": "mfma", "kernel": "w4 MLP weight-gradient pair, standalone",
+        roof = {"bound": "mfma", "kernel": "MLP weight-gradient pair (ping-pong kernel), standalone",
                 "achieved": round(k_tflops, 1), "peak": round(PEAK_BF16_TFLOPS, 1), "unit": "TFLOP/s",
                 "frac": round(k_tflops / PEAK_BF16_TFLOPS, 4), "traffic": traffic, "kernel_ms": round(k_ms, 4),
                 "flop_per_launch": k_flop}

@@ -1316,7 +1316,9 @@ static int pick_variant(int pl, int ql, int M, int N, int R, int split, bool act
   int v;
   if (g_variant >= 0) v = g_variant % 100;
   else if (o >= 0) v = o;
-  else if (wgrad) v = 11;  // wgrad: 4 waves of 128x128 (w4, round 5; 8 = the round-1..4 ping-pong kernel)
+  else if (wgrad) v = 8;   // wgrad: the ping-pong 256x256 kernel; 11 = w4 (4 waves of 128x128, round 5):
+                           // 1.3x the ping-pong's loop ceiling but not faster with loads and epilogue, and
+                           // -0.3 % in the step (profiles/r05/ab_wgrad_w4_vs_pingpong.txt, bench_wgrad_r05a.jsonl)
   else if (fwd) v = 5;     // forward: V5 (the N, R < 1536 proj / patch embedding too: +0.35 % over V2, round 3)
   else v = (act_bwd || (N <= 1024 && R <= 1024)) ? 1 : 3;  // dgrad (GELU' epilogue: V1, 2 WG/CU)
   // (round 5 removed the per-shape overrides VIT_GEMM_{FWD,DGRAD}_{SMALL,GELU}: every re-check measured
