@@ -6,7 +6,10 @@ Backward stamps: 0 start, 1 prologue (Q/dO images, delta) done, 2 phase 1 (dK/dV
                  3 K image written, 4 phase 2 (dQ) + bias partials done, 6 stores drained.
 Slot 5 / 7 hold s_memrealtime (100 MHz) at start / end.
 
-    python tools/attn_stamps.py [--batch 256] [--n 197]
+    python tools/attn_stamps.py [--batch 256] [--n 197] [--variant 1]
+
+--variant selects the backward form (vit_sdpa_bwd_variant); "bwd_us" is the standalone backward time
+(HIP events, mean of 50 launches after warm-up); the two-kernel form (2) records no stamps.
 """
 import argparse
 import ctypes
@@ -47,6 +50,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--n", type=int, default=197)
+    ap.add_argument("--variant", type=int, default=-1)
     a = ap.parse_args()
     B, N, H = a.batch, a.n, 12
     D = H * 64
@@ -59,8 +63,18 @@ def main():
     dbias = torch.empty(3 * D, device=dev)
     lib = L.lib()
     lib.vit_debug_attn_stamps.argtypes = [ctypes.c_void_p]
+    assert lib.vit_sdpa_bwd_variant(a.variant) == 0
     buf = torch.zeros(B * H * 8, dtype=torch.int64, device=dev)
-    res = {"N": N, "batch": B}
+    res = {"N": N, "batch": B, "variant": a.variant}
+    for _ in range(10):
+        ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dqkv=dq, dbias=dbias)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(50):
+        ops.sdpa_bwd(qkv, o, do, lse, B, H, N, dqkv=dq, dbias=dbias)
+    e1.record()
+    torch.cuda.synchronize()
+    res["bwd_us"] = round(e0.elapsed_time(e1) * 1e3 / 50, 1)
     buf.zero_()
     for name, fn, names in (
             ("fwd", lambda: ops.sdpa_fwd(qkv, B, H, N, o=o), [(1, "kv_load"), (2, "compute"), (6, "drain")]),
