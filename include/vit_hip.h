@@ -35,8 +35,9 @@ enum {
   VIT_EPI_QGELU_BWD = 6
 };
 
-int vit_abi_version(void); /* 8 (round 5): vit_gemm_ms / vit_gemm_ms_config and the banded attention
-                              * backward removed; the weight-gradient GEMMs on the w4 kernel */
+int vit_abi_version(void); /* 9 (round 5): vit_blaslt_workspace / vit_gemm_lib (the plain bf16 input
+                              * gradients on hipBLASLt); 8: vit_gemm_ms / vit_gemm_ms_config and the banded
+                              * attention backward removed */
 
 /* Generic MFMA GEMM C[i][j] = epi(sum_r P(i,r) Q(j,r)); layouts RC (r contiguous)
  * or CR (i/j contiguous).  Backs every nn.Linear of timm's ViT reached from
@@ -60,6 +61,19 @@ int vit_gemm_group(int fwd, int dgrad);
  * tiles combine in-launch in a fixed order.  part == NULL removes the stream's entry (host-only); past
  * 32 registered streams a new stream keeps the plain launch. */
 int vit_gemm_streamk_workspace(void* stream, float* part, int64_t part_bytes, int* counters, int ncounters);
+
+/* hipBLASLt for the plain bf16 GEMMs (no fused epilogue beyond a bias; csrc/blaslt.hip): registers the
+ * current device's hipBLASLt handle (created on the first call) and `stream`'s workspace (device memory
+ * the caller owns, >= 32 MiB; ws == NULL unregisters the stream).  A GEMM on an unregistered stream, or
+ * whose shape is first seen during graph capture, runs the hand-written kernels.  By default it takes
+ * the plain vit_linear_fwd (bf16 in / out, EPI_STORE, f32 bias) and vit_linear_dgrad (bf16, EPI_STORE,
+ * no dbias): bit-identical results, +2.6 % step rate (profiles/r05/ab_hipblaslt.txt). */
+int vit_blaslt_workspace(void* stream, void* ws, int64_t bytes);
+
+/* Tuning hook: the GEMM classes that run on hipBLASLt once a stream is registered: bit 0 the plain
+ * bf16 forward (+ f32 bias), bit 1 the plain bf16 input gradient; -1 = from VIT_GEMM_LIB (default 3).
+ * Returns the mask in force. */
+int vit_gemm_lib(int mask);
 
 /* Host-only query (no GPU call): rows per launch the bf16 MFMA path uses for a row-contiguous
  * operand of M rows x ld elements (its staging offsets are 32-bit: larger operands are split

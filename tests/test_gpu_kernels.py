@@ -547,6 +547,39 @@ def test_gemm_splitk_slab_room_exact(R):
     _close(c.cpu(), (Pm.double() @ Qm.double().t()).float(), 1e-5, f"splitk R={R}")
 
 
+@pytest.mark.parametrize("M", [50432, 4096, 1000])
+@pytest.mark.parametrize("N,K", [(2304, 768), (768, 768), (768, 3072)])
+def test_blaslt_plain_gemms_match_kernels(M, N, K):
+    """The plain bf16 input gradient and forward + f32 bias on hipBLASLt
+    (csrc/blaslt.hip, vit_gemm_lib) against the hand-written kernels on the same operands, and both against
+    an fp64 reference: within bf16 output rounding (f32 accumulation in both; the library's k order may
+    differ).  Records whether the two agree bit for bit (they did at every shape here on the box)."""
+    lib = L.lib()
+    bf = torch.bfloat16
+    dy = _rnd(M, N, seed=M + N).to(bf).to(DEV)
+    x = _rnd(M, K, seed=M + K + 1).to(bf).to(DEV)
+    w = (_rnd(N, K, seed=N * K) * 0.05).to(bf).to(DEV)
+    b = _rnd(N, seed=7).to(DEV)
+    outs = {}
+    try:
+        for mask in (0, 3):
+            assert lib.vit_gemm_lib(mask) == mask
+            outs[mask] = (ops.linear_dgrad(dy, w, out_dtype=bf), ops.linear_fwd(x, w, b))
+            torch.cuda.synchronize()
+    finally:
+        lib.vit_gemm_lib(-1)
+    assert lib.vit_gemm_lib(-1) == 3  # the default: both classes
+    ref_d = (dy.double() @ w.double()).float()
+    ref_f = (x.double() @ w.double().t() + b.double()).float()
+    for mask in (0, 3):
+        _close(outs[mask][0], ref_d, 8e-3, f"dgrad mask {mask}")
+        _close(outs[mask][1], ref_f, 8e-3, f"fwd mask {mask}")
+    _close(outs[3][0], outs[0][0], 8e-3, "dgrad: hipBLASLt vs kernel")
+    _close(outs[3][1], outs[0][1], 8e-3, "fwd: hipBLASLt vs kernel")
+    print(f"M={M} N={N} K={K}: dgrad bitwise {torch.equal(outs[3][0], outs[0][0])}, "
+          f"fwd bitwise {torch.equal(outs[3][1], outs[0][1])}")
+
+
 # ---------------------------------------------------------------------------- LayerNorm
 
 @pytest.mark.parametrize("D", [768, 1024, 64, 200])

@@ -876,6 +876,24 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
   gemm_tile<C, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, r_chunk, e, xcd_remap(blockIdx.x, gridDim.x), smem);
 }
 
+// Banded form (lab switch VIT_GEMM_BAND=<per>, input gradients only): workgroup b runs the `per`
+// consecutive tiles b*per .. b*per+per-1 of the row-major walk (one 128- or 256-row band across the
+// N = 768 output columns when per = the column-tile count), so the launch holds total/per workgroups.
+template <class C, int PL, int QL, int EPI, typename TO, typename TA>
+__global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel_band(const bf16* __restrict__ P, int64_t ldp,
+                                                                       const bf16* __restrict__ Q, int64_t ldq,
+                                                                       int M, int N, int R, int r_chunk, Epi e,
+                                                                       int per, int total) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int b = xcd_remap(blockIdx.x, gridDim.x);
+  for (int i = 0; i < per; ++i) {
+    const int w = b * per + i;
+    if (w >= total) break;
+    if (i) __syncthreads();  // the previous tile's LDS (ring / epilogue image) is no longer read
+    gemm_tile<C, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, r_chunk, e, w, smem);
+  }
+}
+
 // ----------------------------------------------------------------------------
 // Ping-pong schedule: 256x256 tile, BK = 32, 8 waves in two groups of four
 // (group g owns rows g*128..g*128+127; wave w%4 owns 64 columns).  Each k-tile is
@@ -1353,6 +1371,23 @@ static int launch_big(const void* P, int64_t ldp, const void* Q, int64_t ldq, in
   const int r_chunk = r_chunk_for(R, split, 64);  // one chunking for every variant (wgrad counts slabs)
   const int nz = (R + r_chunk - 1) / r_chunk;
   dim3 grid(((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN) * nz);
+  if constexpr (PL == LAY_RC && QL == LAY_CR) {
+    static const int band = [] { const char* v = getenv("VIT_GEMM_BAND"); return v ? atoi(v) : 0; }();
+    if (band > 1 && nz == 1) {
+      static bool attr_b = false;
+      if (!attr_b) {
+        (void)hipFuncSetAttribute((const void*)big::gemm_kernel_band<C, PL, QL, EPI, TO, TA>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        attr_b = true;
+      }
+      const int total = (int)grid.x;
+      hipLaunchKernelGGL((big::gemm_kernel_band<C, PL, QL, EPI, TO, TA>), dim3((total + band - 1) / band),
+                         dim3(C::THREADS), lds, s, (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, r_chunk, e,
+                         band, total);
+      VIT_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   hipLaunchKernelGGL((big::gemm_kernel<C, PL, QL, EPI, TO, TA>), grid, dim3(C::THREADS), lds, s,
                      (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, r_chunk, e);
   VIT_CHECK_LAUNCH();
@@ -1623,6 +1658,12 @@ static int gemm_any(int epi, int dtype, int out_dtype, int pl, int ql, int M, in
 
 static Epi make_epi() { Epi e; memset(&e, 0, sizeof(e)); e.dbg = g_dbg; return e; }
 
+// blaslt.hip: plain bf16 GEMMs on hipBLASLt when selected and registered (-1 = not taken)
+int vit_lt_linear_fwd(int M, int N, int K, const void* X, int64_t ldx, const void* W, const float* bias, void* Y,
+                      int64_t ldy, hipStream_t s);
+int vit_lt_linear_dgrad(int M, int N, int K, const void* dY, int64_t lddy, const void* W, void* dX, int64_t lddx,
+                        hipStream_t s);
+
 extern "C" {
 
 // Host-side plan of the bf16 MFMA path's 32-bit staging offsets (no GPU needed; tests):
@@ -1705,6 +1746,10 @@ int vit_gemm_splitk(int p_layout, int q_layout, int M, int N, int R, const float
 int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const void* X, int64_t ldx,
                    const void* W, const float* bias, void* Y, int64_t ldy, const void* resid,
                    void* act_out, void* stream) {
+  if (dtype == VIT_BF16 && out_dtype == VIT_BF16 && epi == EPI_STORE) {  // plain: hipBLASLt if selected (blaslt.hip)
+    const int rc = vit_lt_linear_fwd(M, N, K, X, ldx, W, bias, Y, ldy, (hipStream_t)stream);
+    if (rc != -1) return rc;
+  }
   Epi e = make_epi();
   e.C = Y; e.ldc = ldy; e.bias = bias; e.aux = resid; e.ld_aux = ldy; e.aux_out = act_out;
   return gemm_any(epi, dtype, out_dtype, LAY_RC, LAY_RC, M, N, K, X, ldx, W, K, 1, e, (hipStream_t)stream);
@@ -1724,6 +1769,10 @@ int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, con
                      const void* W, void* dX, int64_t lddx, const void* pre, float* dbias, float* partial,
                      int64_t partial_floats, int defer_reduce, void* stream) {
   hipStream_t s = (hipStream_t)stream;
+  if (dtype == VIT_BF16 && out_dtype == VIT_BF16 && epi == EPI_STORE && !dbias) {  // plain: hipBLASLt if selected
+    const int rc = vit_lt_linear_dgrad(M, N, K, dY, lddy, W, dX, lddx, s);
+    if (rc != -1) return rc;
+  }
   Epi e = make_epi();
   e.C = dX; e.ldc = lddx; e.aux = pre; e.ld_aux = lddx;
   const int rows = (M + 63) / 64;
