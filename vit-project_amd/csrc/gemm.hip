@@ -876,24 +876,6 @@ __global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel(const bf16* __
   gemm_tile<C, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, r_chunk, e, xcd_remap(blockIdx.x, gridDim.x), smem);
 }
 
-// Banded form (lab switch VIT_GEMM_BAND=<per>, input gradients only): workgroup b runs the `per`
-// consecutive tiles b*per .. b*per+per-1 of the row-major walk (one 128- or 256-row band across the
-// N = 768 output columns when per = the column-tile count), so the launch holds total/per workgroups.
-template <class C, int PL, int QL, int EPI, typename TO, typename TA>
-__global__ __launch_bounds__(C::THREADS, C::OCC) void gemm_kernel_band(const bf16* __restrict__ P, int64_t ldp,
-                                                                       const bf16* __restrict__ Q, int64_t ldq,
-                                                                       int M, int N, int R, int r_chunk, Epi e,
-                                                                       int per, int total) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int b = xcd_remap(blockIdx.x, gridDim.x);
-  for (int i = 0; i < per; ++i) {
-    const int w = b * per + i;
-    if (w >= total) break;
-    if (i) __syncthreads();  // the previous tile's LDS (ring / epilogue image) is no longer read
-    gemm_tile<C, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, r_chunk, e, w, smem);
-  }
-}
-
 // ----------------------------------------------------------------------------
 // Ping-pong schedule: 256x256 tile, BK = 32, 8 waves in two groups of four
 // (group g owns rows g*128..g*128+127; wave w%4 owns 64 columns).  Each k-tile is
@@ -1371,23 +1353,6 @@ static int launch_big(const void* P, int64_t ldp, const void* Q, int64_t ldq, in
   const int r_chunk = r_chunk_for(R, split, 64);  // one chunking for every variant (wgrad counts slabs)
   const int nz = (R + r_chunk - 1) / r_chunk;
   dim3 grid(((M + C::BM - 1) / C::BM) * ((N + C::BN - 1) / C::BN) * nz);
-  if constexpr (PL == LAY_RC && QL == LAY_CR) {
-    static const int band = [] { const char* v = getenv("VIT_GEMM_BAND"); return v ? atoi(v) : 0; }();
-    if (band > 1 && nz == 1) {
-      static bool attr_b = false;
-      if (!attr_b) {
-        (void)hipFuncSetAttribute((const void*)big::gemm_kernel_band<C, PL, QL, EPI, TO, TA>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        attr_b = true;
-      }
-      const int total = (int)grid.x;
-      hipLaunchKernelGGL((big::gemm_kernel_band<C, PL, QL, EPI, TO, TA>), dim3((total + band - 1) / band),
-                         dim3(C::THREADS), lds, s, (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, r_chunk, e,
-                         band, total);
-      VIT_CHECK_LAUNCH();
-      return 0;
-    }
-  }
   hipLaunchKernelGGL((big::gemm_kernel<C, PL, QL, EPI, TO, TA>), grid, dim3(C::THREADS), lds, s,
                      (const bf16*)P, ldp, (const bf16*)Q, ldq, M, N, R, r_chunk, e);
   VIT_CHECK_LAUNCH();
