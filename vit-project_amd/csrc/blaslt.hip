@@ -8,7 +8,9 @@
 // the input gradients as one workgroup per 256-row band walking the N = 768 output columns
 // (197 workgroups at bs=256): beside the side stream's weight gradients they hold fewer CUs than our
 // 2-workgroup-per-CU V3 / V1 launches (1182 workgroups).  Everything with a fused epilogue (GELU pair,
-// GELU', residual, column sums, split-K slabs, stream-K f32) stays on the kernels in gemm.hip.
+// GELU', residual, column sums, split-K slabs, stream-K f32) stays on the kernels in gemm.hip, and so do
+// the weight gradients: the library's f32-output dW GEMMs ran 228-591 vs 596-841 TFLOP/s and -10.7 % in
+// the step (profiles/r05/hipblaslt_wgrad_negative.txt).
 //
 // Column-major mapping (hipBLASLt is column-major; our matrices are row-major):
 //   dgrad  dX[M,K] = dY[M,N] W[N,K]      ->  dX^T (K x M) = W^T (K x N, "A", op N) * dY^T (N x M, "B", op N)
@@ -87,7 +89,7 @@ const LtPlan* lt_plan(int dev, int kind, int m, int n, int k, int64_t lda, int64
     ok = ok && hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_BIAS_DATA_TYPE, &bt, sizeof(bt)) ==
                    HIPBLAS_STATUS_SUCCESS;
   }
-  // A: kind 0 stored K x N (ld k = lda) read transposed; kind 1 stored m x k = K x N (ld lda)
+  // A: kind 0 stored K x N (ld lda) read transposed; kind 1 stored m x k = K x N (ld lda).  B: k x n.
   const uint64_t ar = kind == 0 ? (uint64_t)k : (uint64_t)m, ac = kind == 0 ? (uint64_t)m : (uint64_t)k;
   ok = ok && hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16BF, ar, ac, lda) == HIPBLAS_STATUS_SUCCESS;
   ok = ok && hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16BF, (uint64_t)k, (uint64_t)n, ldb) == HIPBLAS_STATUS_SUCCESS;
@@ -118,7 +120,7 @@ const LtPlan* lt_plan(int dev, int kind, int m, int n, int k, int64_t lda, int64
 // 0 = done on the library; -1 = not taken (the caller runs its own kernel); else a hip error
 int lt_run(int kind, int m, int n, int k, const void* A, int64_t lda, const void* B, int64_t ldb, void* C,
            int64_t ldc, const float* bias, hipStream_t s) {
-  if (!(lt_mask() & (kind == 0 ? 1 : 2))) return -1;
+  if (!(lt_mask() & (1 << kind))) return -1;
   if (m <= 0 || n <= 0 || k <= 0) return -1;
   const int dev = cur_device();
   if (dev < 0 || dev >= LT_MAX_DEV || !g_lt[dev]) return -1;
