@@ -39,6 +39,8 @@ LABELS = [  # (regex on the mangled name, label)
     (r"CfgILi128ELi256ELi32E.*ELi0ELi1ELi0E", "dgrad: V3 128x256x32 (fc1, qkv)"),
     (r"CfgILi256ELi128ELi32E.*ELi0ELi1ELi3E", "dgrad: V1 256x128x32 GELU' (fc2)"),
     (r"CfgILi256ELi128ELi32E.*ELi0ELi1ELi0E", "dgrad: V1 256x128x32 (proj)"),
+    (r"Cijk_Alik", "fwd: hipBLASLt plain + bias (qkv, proj, fc2)"),
+    (r"Cijk_Ailk", "dgrad: hipBLASLt plain (qkv, fc1, proj)"),
     (r"attn_fwd", "attention fwd"),
     (r"attn_bwd", "attention bwd"),
     (r"ln_bwd_kernel", "layernorm bwd"),
