@@ -18,7 +18,7 @@ if not f: print("no counter csv", sys.argv[1]); sys.exit(0)
 rows = list(csv.DictReader(open(f[0])))
 agg = collections.defaultdict(lambda: collections.defaultdict(float))
 for r in rows:
-    if "gemm" not in r["Kernel_Name"] and "pp_kernel" not in r["Kernel_Name"]: continue
+    if "gemm" not in r["Kernel_Name"] and "pp_kernel" not in r["Kernel_Name"] and "w4" not in r["Kernel_Name"]: continue
     agg[r["Kernel_Name"][:60]][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, d in agg.items():
     print(sys.argv[1].split("/")[-1], k, {a: int(b) for a, b in d.items()})
