@@ -50,8 +50,10 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
 int vit_gemm_variant(int v);
 
 /* Tuning hook: the forward / input-gradient GEMMs walk their tiles in bands of `fwd` / `dgrad`
- * row tiles, column-major inside a band (L2 reuse of the weight columns); 0 = row-major (the
- * default), -1 = the per-shape rule (bands of 8 for wide outputs with >= 4 MiB weights). */
+ * row tiles, column-major inside a band (L2 reuse of the operand blocks); 0 = row-major (the forward
+ * default), -1 = the per-shape rule (bands of 8 for wide outputs with >= 4 MiB weights).  The input
+ * gradients default to bands of 4 (round 5: the fc2 GELU' one, 3.9x less operand FETCH, +0.65 %);
+ * -2 restores a class's default (VIT_GEMM_GROUP_FWD / _DGRAD, else the defaults above). */
 int vit_gemm_group(int fwd, int dgrad);
 
 /* Stream-K workspace for the fp32 MFMA GEMMs launched on `stream` (the reference-precision C3 path,

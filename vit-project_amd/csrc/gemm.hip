@@ -1411,12 +1411,15 @@ static int num_cus() {
 // Bands of 8 row tiles help the wide-output GEMMs whose weight operand does not fit beside the
 // row blocks in an XCD's 4 MiB L2 (the fc1 forward GELU pair and the fc2 GELU' input gradient:
 // +3.5-4.5 % standalone at the half-batch shapes, tools/bench_kernels.py --groups) but measured
-// 0.5-1 % slower in the two-stream step (profiles/r03/ab_group_colbatch.txt), so the default is
-// the row-major walk; -1 selects that per-shape band rule.
+// 0.5-1 % slower in the two-stream step (profiles/r03/ab_group_colbatch.txt), so the forward keeps
+// the row-major walk; -1 selects that per-shape band rule.  Round 5: with the plain input gradients
+// on hipBLASLt the only input gradient left here is fc2's GELU' one, and bands of 4 row tiles cut its
+// operand FETCH from 288 to 74 MB raw (profiles/r05/pmc_fc2_gelu_dgrad_bands.json) and measured +0.65 %
+// in the step (profiles/r05/ab_dgrad_band4.txt): the input-gradient default is 4.
 static int g_group[2] = {-2, -2};  // forward, dgrad; -2 = not yet read from the environment
 static int group_for(int pl, int ql, int N, int R) {
   if (g_group[0] == -2) { const int v = env_variant("VIT_GEMM_GROUP_FWD"); g_group[0] = v == -1 ? 0 : v; }
-  if (g_group[1] == -2) { const int v = env_variant("VIT_GEMM_GROUP_DGRAD"); g_group[1] = v == -1 ? 0 : v; }
+  if (g_group[1] == -2) { const int v = env_variant("VIT_GEMM_GROUP_DGRAD"); g_group[1] = v == -1 ? 4 : v; }
   const int g = (pl == LAY_RC && ql == LAY_RC) ? g_group[0] : (pl == LAY_RC && ql == LAY_CR) ? g_group[1] : 0;
   if (g >= 0) return g;
   return (N >= 2048 && (int64_t)N * R * 2 >= ((int64_t)4 << 20)) ? 8 : 0;
