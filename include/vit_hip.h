@@ -35,9 +35,10 @@ enum {
   VIT_EPI_QGELU_BWD = 6
 };
 
-int vit_abi_version(void); /* 9 (round 5): vit_blaslt_workspace / vit_gemm_lib (the plain bf16 input
-                              * gradients on hipBLASLt); 8: vit_gemm_ms / vit_gemm_ms_config and the banded
-                              * attention backward removed */
+int vit_abi_version(void); /* 10 (round 6): vit_blaslt_workspace / vit_gemm_lib removed -- the plain bf16
+                              * forward / input-gradient GEMMs run the hand-written 4-wave kernel (csrc/
+                              * gemm_g4.hip), the library links no vendor BLAS; 9: those two hooks (hipBLASLt);
+                              * 8: vit_gemm_ms / vit_gemm_ms_config and the banded attention backward removed */
 
 /* Generic MFMA GEMM C[i][j] = epi(sum_r P(i,r) Q(j,r)); layouts RC (r contiguous)
  * or CR (i/j contiguous).  Backs every nn.Linear of timm's ViT reached from
@@ -46,7 +47,9 @@ int vit_gemm(int dtype, int out_dtype, int p_layout, int q_layout, int epi, int 
              const void* P, int64_t ldp, const void* Q, int64_t ldq, void* C, int64_t ldc,
              const float* bias, const void* aux, int64_t ld_aux, void* aux_out, int allow_fast, void* stream);
 
-/* Tuning hook: force GEMM tile configuration v (see csrc/gemm.hip big::V*), -1 = per-shape choice. */
+/* Tuning hook: force GEMM tile configuration v (see csrc/gemm.hip big::V*; 20 = the 4-wave g4 kernel of
+ * csrc/gemm_g4.hip for the plain bf16 store classes), -1 = per-shape choice (g4 for the plain bf16
+ * forward / input gradient unless VIT_GEMM_G4=0). */
 int vit_gemm_variant(int v);
 
 /* Tuning hook: the forward / input-gradient GEMMs walk their tiles in bands of `fwd` / `dgrad`
@@ -56,6 +59,16 @@ int vit_gemm_variant(int v);
  * -2 restores a class's default (VIT_GEMM_GROUP_FWD / _DGRAD, else the defaults above). */
 int vit_gemm_group(int fwd, int dgrad);
 
+/* The plain bf16 forward (+ f32 bias) and input-gradient GEMMs run the 4-wave g4 kernel (csrc/gemm_g4.hip,
+ * VIT:139 / VIT:142 through timm's qkv / proj / fc1 / fc2).  Tuning / test hook: its tile walk for the forward
+ * and the input-gradient class (0 = stride over the tiles with min(tiles, CUs or `wgs`) persistent workgroups,
+ * 1 = one workgroup per 256-row band walking the column tiles, -1 = keep) and the stride walk's workgroup cap
+ * (0 = the CU count, -1 = keep). */
+int vit_gemm_g4_config(int fwd_mode, int dgrad_mode, int wgs);
+
+/* Host-side count of g4 launches since the last reset (reset != 0 zeroes it); no GPU call. */
+int vit_gemm_g4_count(int reset);
+
 /* Stream-K workspace for the fp32 MFMA GEMMs launched on `stream` (the reference-precision C3 path,
  * NEWP:274): part >= 4 * CUs * 128*128 floats, counters >= 2 * CUs ints, zero-filled before first use
  * (kernels leave them zero).  With it, an f32 GEMM whose tile count would leave a ragged last round
@@ -63,19 +76,6 @@ int vit_gemm_group(int fwd, int dgrad);
  * tiles combine in-launch in a fixed order.  part == NULL removes the stream's entry (host-only); past
  * 32 registered streams a new stream keeps the plain launch. */
 int vit_gemm_streamk_workspace(void* stream, float* part, int64_t part_bytes, int* counters, int ncounters);
-
-/* hipBLASLt for the plain bf16 GEMMs (no fused epilogue beyond a bias; csrc/blaslt.hip): registers the
- * current device's hipBLASLt handle (created on the first call) and `stream`'s workspace (device memory
- * the caller owns, >= 32 MiB; ws == NULL unregisters the stream).  A GEMM on an unregistered stream, or
- * whose shape is first seen during graph capture, runs the hand-written kernels.  By default it takes
- * the plain vit_linear_fwd (bf16 in / out, EPI_STORE, f32 bias) and vit_linear_dgrad (bf16, EPI_STORE,
- * no dbias): bit-identical results, +2.6 % step rate (profiles/r05/ab_hipblaslt.txt). */
-int vit_blaslt_workspace(void* stream, void* ws, int64_t bytes);
-
-/* Tuning hook: the GEMM classes that run on hipBLASLt once a stream is registered: bit 0 the plain
- * bf16 forward (+ f32 bias), bit 1 the plain bf16 input gradient; -1 = from VIT_GEMM_LIB (default 3).
- * Returns the mask in force. */
-int vit_gemm_lib(int mask);
 
 /* Host-only query (no GPU call): rows per launch the bf16 MFMA path uses for a row-contiguous
  * operand of M rows x ld elements (its staging offsets are 32-bit: larger operands are split

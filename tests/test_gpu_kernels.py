@@ -547,37 +547,77 @@ def test_gemm_splitk_slab_room_exact(R):
     _close(c.cpu(), (Pm.double() @ Qm.double().t()).float(), 1e-5, f"splitk R={R}")
 
 
-@pytest.mark.parametrize("M", [50432, 4096, 1000])
-@pytest.mark.parametrize("N,K", [(2304, 768), (768, 768), (768, 3072)])
-def test_blaslt_plain_gemms_match_kernels(M, N, K):
-    """The plain bf16 input gradient and forward + f32 bias on hipBLASLt
-    (csrc/blaslt.hip, vit_gemm_lib) against the hand-written kernels on the same operands, and both against
-    an fp64 reference: within bf16 output rounding (f32 accumulation in both; the library's k order may
-    differ).  Records whether the two agree bit for bit (they did at every shape here on the box)."""
+def _g4_pair(x, w, b, dy, variant=-1):
+    """(forward + bias, input gradient) through ops with GEMM variant `variant` forced (-1 = default)."""
+    lib = L.lib()
+    lib.vit_gemm_variant(variant)
+    try:
+        y = ops.linear_fwd(x, w, b)
+        d = ops.linear_dgrad(dy, w, out_dtype=torch.bfloat16)
+        torch.cuda.synchronize()
+    finally:
+        lib.vit_gemm_variant(-1)
+    return y, d
+
+
+@pytest.mark.parametrize("M", [50432, 27580, 22852, 1000])
+@pytest.mark.parametrize("N,K", [(2304, 768), (768, 768), (768, 3072), (3072, 768)])
+def test_g4_plain_gemms_bitwise_match_8wave_kernels(M, N, K):
+    """The plain bf16 forward + f32 bias and input gradient on the 4-wave g4 kernel (csrc/gemm_g4.hip, the
+    default since round 6) at the step's shapes -- the full batch and the two forward chains' row counts
+    (140 / 116 images) -- against the 8-wave kernels forced (V5 forward, V1 input gradient): the same k order
+    (32-deep MFMA chunks in sequence) and the same epilogue arithmetic, so they agree BIT FOR BIT; both
+    against an fp64 reference within bf16 output rounding.  The launch counter confirms g4 ran."""
     lib = L.lib()
     bf = torch.bfloat16
     dy = _rnd(M, N, seed=M + N).to(bf).to(DEV)
     x = _rnd(M, K, seed=M + K + 1).to(bf).to(DEV)
     w = (_rnd(N, K, seed=N * K) * 0.05).to(bf).to(DEV)
     b = _rnd(N, seed=7).to(DEV)
-    outs = {}
+    lib.vit_gemm_g4_count(1)
+    y4, d4 = _g4_pair(x, w, b, dy)
+    assert lib.vit_gemm_g4_count(1) == 2, "the plain GEMMs did not run on g4"
+    y5, _ = _g4_pair(x, w, b, dy, variant=5)
+    _, d1 = _g4_pair(x, w, b, dy, variant=1)
+    assert lib.vit_gemm_g4_count(1) == 0
+    assert torch.equal(y4, y5), "g4 forward differs from V5"
+    assert torch.equal(d4, d1), "g4 input gradient differs from V1"
+    _close(d4, (dy.double() @ w.double()).float(), 8e-3, "g4 dgrad vs fp64")
+    _close(y4, (x.double() @ w.double().t() + b.double()).float(), 8e-3, "g4 fwd vs fp64")
+
+
+@pytest.mark.parametrize("fwd_mode,dgrad_mode,wgs", [(0, 1, 0), (1, 0, 0), (0, 0, 7), (0, 0, 1), (1, 1, 0)])
+@pytest.mark.parametrize("M,N,K", [(1, 64, 64), (257, 136, 192), (197 * 3, 640, 448), (2000, 1088, 64),
+                                   (513, 256, 3072), (300, 8, 128)])
+def test_g4_tile_walks_and_ragged_shapes(fwd_mode, dgrad_mode, wgs, M, N, K):
+    """Every tile walk (stride over G persistent workgroups, G = CUs / 7 / 1 -- one workgroup running every
+    tile in sequence -- and the row-band walk) on ragged shapes: M = 1 and 257 (a 1-row last tile), output
+    widths 8 / 136 / 448 / 1088 (partial 8-column chunks of the last column tile), a single k-step (K = 64)
+    and long reductions; the stage stream crosses tile boundaries with 1..48 k-steps per tile.  The forward
+    runs on g4 whenever K % 64 == 0 and N % 8 == 0, the input gradient (reduction N) when N % 64 == 0;
+    where g4 ran it is bitwise equal to the 8-wave kernels, and everything is within bf16 rounding of fp64."""
+    lib = L.lib()
+    bf = torch.bfloat16
+    dy = _rnd(M, N, seed=3 * M + N).to(bf).to(DEV)
+    x = _rnd(M, K, seed=M + 5 * K).to(bf).to(DEV)
+    w = (_rnd(N, K, seed=N + K) * 0.05).to(bf).to(DEV)
+    b = _rnd(N, seed=8).to(DEV)
+    fwd_g4, dgrad_g4 = K % 64 == 0 and N % 8 == 0, N % 64 == 0 and K % 8 == 0
+    lib.vit_gemm_g4_config(fwd_mode, dgrad_mode, wgs)
     try:
-        for mask in (0, 3):
-            assert lib.vit_gemm_lib(mask) == mask
-            outs[mask] = (ops.linear_dgrad(dy, w, out_dtype=bf), ops.linear_fwd(x, w, b))
-            torch.cuda.synchronize()
+        lib.vit_gemm_g4_count(1)
+        y4, d4 = _g4_pair(x, w, b, dy)
+        assert lib.vit_gemm_g4_count(1) == int(fwd_g4) + int(dgrad_g4)
     finally:
-        lib.vit_gemm_lib(-1)
-    assert lib.vit_gemm_lib(-1) == 3  # the default: both classes
-    ref_d = (dy.double() @ w.double()).float()
-    ref_f = (x.double() @ w.double().t() + b.double()).float()
-    for mask in (0, 3):
-        _close(outs[mask][0], ref_d, 8e-3, f"dgrad mask {mask}")
-        _close(outs[mask][1], ref_f, 8e-3, f"fwd mask {mask}")
-    _close(outs[3][0], outs[0][0], 8e-3, "dgrad: hipBLASLt vs kernel")
-    _close(outs[3][1], outs[0][1], 8e-3, "fwd: hipBLASLt vs kernel")
-    print(f"M={M} N={N} K={K}: dgrad bitwise {torch.equal(outs[3][0], outs[0][0])}, "
-          f"fwd bitwise {torch.equal(outs[3][1], outs[0][1])}")
+        lib.vit_gemm_g4_config(0, 1, 0)
+    y5, _ = _g4_pair(x, w, b, dy, variant=5)
+    _, d1 = _g4_pair(x, w, b, dy, variant=1)
+    if fwd_g4:
+        assert torch.equal(y4, y5), "g4 forward differs from V5"
+    if dgrad_g4:
+        assert torch.equal(d4, d1), "g4 input gradient differs from V1"
+    _close(y4, (x.double() @ w.double().t() + b.double()).float(), 8e-3, "g4 fwd vs fp64")
+    _close(d4, (dy.double() @ w.double()).float(), 8e-3, "g4 dgrad vs fp64")
 
 
 # ---------------------------------------------------------------------------- LayerNorm

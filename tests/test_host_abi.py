@@ -28,7 +28,7 @@ def test_library_exports_every_header_symbol():
         assert name in _lib.SIGNATURES, f"{name} missing from the ctypes signature table"
     for name in _lib.SIGNATURES:
         assert name in declared, f"{name} bound in Python but not declared in include/vit_hip.h"
-    assert lib.vit_abi_version() == 9
+    assert lib.vit_abi_version() == 10
     assert lib.vit_sgd_tensor_bytes() == 40 and lib.vit_sgd_chunk_bytes() == 16
     assert lib.vit_sgd_chunk_size() == 4096
 

@@ -1,0 +1,94 @@
+"""The plain bf16 GEMM classes of the step on the 4-wave g4 kernel (csrc/gemm_g4.hip) against the 8-wave
+kernels it replaced (V5 forward, V1 / V3 input gradients, forced through vit_gemm_variant) and against
+hipBLASLt behind torch (F.linear with bias / matmul) -- the vendor kernels round 5 dispatched to --
+at the step's shapes: forwards of qkv / proj / fc2 at the two forward chains' row counts (140 / 116
+images), input gradients of qkv / fc1 / proj at the full batch.  Interleaved rounds, HIP events, TFLOP/s.
+
+    python tools/bench_g4.py [--reps 20] [--rounds 2] [--walks]   (--walks: every g4 tile walk too)
+"""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "vit-project_amd"))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from vit_amd import ops, _lib as L  # noqa: E402
+
+
+def timeit(fn, reps):
+    for _ in range(3):
+        fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--walks", action="store_true")
+    ap.add_argument("--shapes", default="")
+    a = ap.parse_args()
+    lib = L.lib()
+    dev, bf = "cuda", torch.bfloat16
+    torch.backends.cuda.preferred_blas_library("hipblaslt")
+    D, Fh = 768, 3072
+    B = 256
+    m_half = (B // 2 + 3 * B // 64) * 197, (B - (B // 2 + 3 * B // 64)) * 197
+    cases = []
+    for M in m_half:
+        for nm, (K, N) in (("qkv", (D, 3 * D)), ("proj", (D, D)), ("fc2", (Fh, D))):
+            cases.append(("fwd", nm, M, N, K))
+    for nm, (N, K) in (("qkv", (3 * D, D)), ("fc1", (Fh, D)), ("proj", (D, D))):
+        cases.append(("dgrad", nm, B * 197, N, K))
+    if a.shapes:
+        keep = set(a.shapes.split(","))
+        cases = [c for c in cases if f"{c[0]}_{c[1]}" in keep]
+    for kind, nm, M, N, K in cases:
+        g = torch.Generator(device=dev).manual_seed(M + N + K)
+        w = (torch.randn(N, K, device=dev, generator=g) * 0.05).to(bf)
+        flop = 2.0 * M * N * K
+        rec = {"class": kind, "shape": nm, "M": M, "N": N, "K": K}
+        if kind == "fwd":
+            x = torch.randn(M, K, device=dev, generator=g).to(bf)
+            b = torch.randn(N, device=dev, generator=g)
+            bb = b.to(bf)
+            y = torch.empty(M, N, device=dev, dtype=bf)
+            ours = lambda: ops.linear_fwd(x, w, b, out=y)  # noqa: E731
+            lib_fn = lambda: F.linear(x, w, bb)  # noqa: E731
+            old = [5]
+        else:
+            dy = torch.randn(M, N, device=dev, generator=g).to(bf)
+            dx = torch.empty(M, K, device=dev, dtype=bf)
+            ours = lambda: ops.linear_dgrad(dy, w, out_dtype=bf, out=dx)  # noqa: E731
+            lib_fn = lambda: torch.matmul(dy, w)  # noqa: E731
+            old = [1, 3]
+        walks = [(0, 1, 0)]
+        if a.walks:
+            walks = [(0, 1, 0), (1, 1, 0), (0, 0, 0)] if kind == "fwd" else [(0, 1, 0), (0, 0, 0)]
+        for _ in range(a.rounds):
+            for wk in walks:
+                lib.vit_gemm_g4_config(*wk)
+                key = "g4" if wk == (0, 1, 0) else f"g4_walk{wk[0] if kind == 'fwd' else wk[1]}"
+                rec.setdefault(key, []).append(round(flop / timeit(ours, a.reps) / 1e12, 1))
+            lib.vit_gemm_g4_config(0, 1, 0)
+            for v in old:
+                lib.vit_gemm_variant(v)
+                rec.setdefault(f"V{v}", []).append(round(flop / timeit(ours, a.reps) / 1e12, 1))
+                lib.vit_gemm_variant(-1)
+            rec.setdefault("hipblaslt", []).append(round(flop / timeit(lib_fn, a.reps) / 1e12, 1))
+        print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -24,6 +24,7 @@
 #include <type_traits>
 
 #include "gemm_lds.hpp"
+#include "gemm_epi.hpp"
 // build-time switches of the bf16 epilogue forms (A/B builds: -DVIT_PAIR16=0 etc.)
 #ifndef VIT_PAIR16
 #define VIT_PAIR16 1
@@ -40,23 +41,6 @@
 #ifndef VIT_SPLIT_ISSUE1
 #define VIT_SPLIT_ISSUE1 1
 #endif
-// BIAS_GELU / BIAS_QGELU: C = act'(pre) (what the backward needs), aux_out = act(pre);
-// GELU_BWD / QGELU_BWD: C = acc * aux, aux = that saved act'(pre)  (same for both).
-enum { EPI_STORE = 0, EPI_BIAS_GELU = 1, EPI_RESID = 2, EPI_GELU_BWD = 3, EPI_PATCH = 4,
-       EPI_BIAS_QGELU = 5, EPI_QGELU_BWD = 6, EPI_ACC = 7 };
-
-struct Epi {
-  void* C; int64_t ldc;
-  const float* bias;        // [N] or null
-  const void* aux; int64_t ld_aux;  // EPI_RESID: f32 residual;  *_BWD: pre-activation (T)
-  void* aux_out;            // BIAS_GELU: activation output (T, ld = ldc)
-  const float* pos;         // EPI_PATCH: pos_embed [seq, N]
-  int n_patch;              // EPI_PATCH: patches per image (seq = n_patch + 1)
-  int64_t slab;             // split-r: element offset of slab z
-  float* csum;              // optional column sums of the epilogue output: [ceil(M/64)][N] partials (64-row groups)
-  int group_m;              // > 0: tiles walk column-major inside bands of group_m row tiles (L2 reuse of Q columns)
-  int dbg;                  // timing experiments only (vit_gemm_variant(v + 100*bits)): 1 = no in-loop loads, 2 = no in-loop barriers, 4 = no epilogue, 16 = fragment epilogue
-};
 
 template <typename T> __device__ __forceinline__ void store4(T* p, f32x4 v);
 template <> __device__ __forceinline__ void store4<float>(float* p, f32x4 v) {
@@ -280,17 +264,6 @@ __device__ __forceinline__ f32x4 epi_val(const Epi& e, int i, int j, f32x4 v, bo
   return v;
 }
 
-__device__ __forceinline__ void store_pair_bf16(void* base, int64_t ldc, int i, int col, const f32x4& x,
-                                                const f32x4& y, bool ok) {
-  const bf16x4 px = {(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
-  const bf16x4 py = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
-  typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-  const u32x2 ux = __builtin_bit_cast(u32x2, px), uy = __builtin_bit_cast(u32x2, py);
-  const auto r0 = __builtin_amdgcn_permlane16_swap(ux[0], uy[0], false, false);
-  const auto r1 = __builtin_amdgcn_permlane16_swap(ux[1], uy[1], false, false);
-  if (ok) *reinterpret_cast<u32x4*>((bf16*)base + (int64_t)i * ldc + col) = u32x4{r0[0], r1[0], r0[1], r1[1]};
-}
 
 template <class C, int EPI, typename TO, typename TA>
 __device__ __forceinline__ void epilogue_swap(const Epi& e, const f32x4 (&acc)[C::AI][C::AJ], int i0, int j0, int wi,
@@ -581,24 +554,6 @@ __device__ __forceinline__ bf16x8 frag(const char* img, int s, int kk, int lane)
   }
 }
 
-
-// Tile t of a tiles_i x tiles_j grid.  group_m == 0: row-major (consecutive t share a row tile,
-// so the P rows stay in the XCD's L2 while every Q column block streams past).  group_m > 0:
-// bands of group_m row tiles walked column-major, so the workgroups an XCD runs at once cover
-// group_m row tiles x a few column tiles and both operand blocks fit its 4 MiB L2.
-__device__ __forceinline__ void tile_coords(int t, int tiles_i, int tiles_j, int group_m, int& ti, int& tj) {
-  if (group_m <= 0) {
-    ti = t / tiles_j;
-    tj = t - ti * tiles_j;
-    return;
-  }
-  const int per = group_m * tiles_j;
-  const int g = t / per, r = t - g * per;
-  const int first = g * group_m;
-  const int gsz = min(tiles_i - first, group_m);
-  tj = r / gsz;
-  ti = first + (r - tj * gsz);
-}
 
 // One output tile (unit w of the 1-D (split, tile) space) of the fast bf16 GEMM.
 template <class C, int PL, int QL, int EPI, typename TO, typename TA>
@@ -1407,6 +1362,12 @@ static int num_cus() {
   }
   return n;
 }
+
+// g4 (gemm_g4.hip): the plain bf16 forward / input-gradient GEMMs.  g4_enabled(): VIT_GEMM_G4=0 sends these
+// classes back to the 8-wave V5 / V1 / V3 kernels (A/B); g4_launch returns -1 for shapes it does not take.
+bool g4_enabled();
+int g4_launch(int q_layout, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
+              const Epi& e, hipStream_t s);
 // row-tile band of the tile walk per class (tile_coords); VIT_GEMM_GROUP_{FWD,DGRAD}=<row tiles> (A/B)
 // Bands of 8 row tiles help the wide-output GEMMs whose weight operand does not fit beside the
 // row blocks in an XCD's 4 MiB L2 (the fc1 forward GELU pair and the fc2 GELU' input gradient:
@@ -1431,6 +1392,14 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
   Epi e = e0;
   if (split <= 1) e.group_m = group_for(PL, QL, N, R);
   const int v = pick_variant(PL, QL, M, N, R, split, EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD);
+  if constexpr (PL == LAY_RC && EPI == EPI_STORE && std::is_same<TO, bf16>::value) {
+    // the plain bf16 forward / input gradient: g4 by default (variant 20 forces it; any other forced
+    // variant, a timing flag or VIT_GEMM_G4=0 keeps the 8-wave kernels)
+    if (v == 20 || (g4_enabled() && g_variant < 0 && !e.dbg)) {
+      const int rc = g4_launch(QL, P, ldp, Q, ldq, M, N, R, split, e, s);
+      if (rc != -1) return rc;
+    }
+  }
   if constexpr (PL == LAY_CR && QL == LAY_CR) {  // w4 ring / load-placement A/B (tools/bench_kernels.py --sweep)
     if (v == 12) return launch_w4<w4::Cfg<4, 0>, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
     if (v == 13) return launch_w4<w4::Cfg<4, 2>, PL, QL, EPI, TO, TA>(P, ldp, Q, ldq, M, N, R, split, e, s);
@@ -1626,12 +1595,6 @@ static int gemm_any(int epi, int dtype, int out_dtype, int pl, int ql, int M, in
 
 static Epi make_epi() { Epi e; memset(&e, 0, sizeof(e)); e.dbg = g_dbg; return e; }
 
-// blaslt.hip: plain bf16 GEMMs on hipBLASLt when selected and registered (-1 = not taken)
-int vit_lt_linear_fwd(int M, int N, int K, const void* X, int64_t ldx, const void* W, const float* bias, void* Y,
-                      int64_t ldy, hipStream_t s);
-int vit_lt_linear_dgrad(int M, int N, int K, const void* dY, int64_t lddy, const void* W, void* dX, int64_t lddx,
-                        hipStream_t s);
-
 extern "C" {
 
 // Host-side plan of the bf16 MFMA path's 32-bit staging offsets (no GPU needed; tests):
@@ -1714,10 +1677,6 @@ int vit_gemm_splitk(int p_layout, int q_layout, int M, int N, int R, const float
 int vit_linear_fwd(int dtype, int out_dtype, int epi, int M, int N, int K, const void* X, int64_t ldx,
                    const void* W, const float* bias, void* Y, int64_t ldy, const void* resid,
                    void* act_out, void* stream) {
-  if (dtype == VIT_BF16 && out_dtype == VIT_BF16 && epi == EPI_STORE) {  // plain: hipBLASLt if selected (blaslt.hip)
-    const int rc = vit_lt_linear_fwd(M, N, K, X, ldx, W, bias, Y, ldy, (hipStream_t)stream);
-    if (rc != -1) return rc;
-  }
   Epi e = make_epi();
   e.C = Y; e.ldc = ldy; e.bias = bias; e.aux = resid; e.ld_aux = ldy; e.aux_out = act_out;
   return gemm_any(epi, dtype, out_dtype, LAY_RC, LAY_RC, M, N, K, X, ldx, W, K, 1, e, (hipStream_t)stream);
@@ -1737,10 +1696,6 @@ int vit_linear_dgrad(int dtype, int out_dtype, int epi, int M, int N, int K, con
                      const void* W, void* dX, int64_t lddx, const void* pre, float* dbias, float* partial,
                      int64_t partial_floats, int defer_reduce, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  if (dtype == VIT_BF16 && out_dtype == VIT_BF16 && epi == EPI_STORE && !dbias) {  // plain: hipBLASLt if selected
-    const int rc = vit_lt_linear_dgrad(M, N, K, dY, lddy, W, dX, lddx, s);
-    if (rc != -1) return rc;
-  }
   Epi e = make_epi();
   e.C = dX; e.ldc = lddx; e.aux = pre; e.ld_aux = lddx;
   const int rows = (M + 63) / 64;

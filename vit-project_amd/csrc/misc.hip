@@ -331,6 +331,6 @@ int vit_zero(void* p, int64_t bytes, void* stream) {
   return (int)hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);
 }
 
-int vit_abi_version(void) { return 9; }
+int vit_abi_version(void) { return 10; }
 
 }  // extern "C"

@@ -27,9 +27,9 @@ SIGNATURES = {
     "vit_abi_version": [],
     "vit_gemm_variant": [i32],
     "vit_gemm_group": [i32, i32],
+    "vit_gemm_g4_config": [i32, i32, i32],
+    "vit_gemm_g4_count": [i32],
     "vit_gemm_streamk_workspace": [vp, vp, i64, vp, i32],
-    "vit_blaslt_workspace": [vp, vp, i64],
-    "vit_gemm_lib": [i32],
     "vit_gemm_rc_chunk_rows": [i32, i64],
     "vit_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, vp],
     "vit_linear_fwd": [i32, i32, i32, i32, i32, i32, vp, i64, vp, vp, vp, i64, vp, vp, vp],

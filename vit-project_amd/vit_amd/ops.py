@@ -72,30 +72,10 @@ def _streamk(device, stream=None):
 
 
 def register_capture_stream(stream, device=None):
-    """Give ``stream`` (e.g. the side stream a ``torch.cuda.graph`` captures on) its stream-K and hipBLASLt
-    workspaces before capture, so the GEMMs captured on it take the same forms -- and the same bits --
-    as the eager launches on a registered stream."""
+    """Give ``stream`` (e.g. the side stream a ``torch.cuda.graph`` captures on) its stream-K workspace
+    before capture, so the f32 GEMMs captured on it take the same form -- and the same bits -- as the
+    eager launches on a registered stream."""
     _streamk(stream.device if device is None else device, stream)
-    _blaslt(stream.device if device is None else device, stream)
-
-
-_LT = {}  # (device index, stream handle) -> workspace registered with vit_blaslt_workspace
-LT_WS_BYTES = 32 << 20
-
-
-def _blaslt(device, stream=None):
-    """Register (once per (device, stream)) the hipBLASLt workspace the plain bf16 GEMMs on that stream use
-    (csrc/blaslt.hip; which classes: vit_gemm_lib).  Not while capturing: a capture stream registered
-    before capture takes the library path inside the graph too (``register_capture_stream``)."""
-    st = L.stream_ptr(device) if stream is None else stream.cuda_stream
-    idx = torch.device(device).index
-    key = (idx if idx is not None else torch.cuda.current_device(), st)
-    if key in _LT or torch.cuda.is_current_stream_capturing():
-        return
-    ws = torch.empty(LT_WS_BYTES, dtype=torch.uint8, device=device)
-    with torch.cuda.device(key[0]):
-        call("vit_blaslt_workspace", st, ptr(ws), ws.numel())
-    _LT[key] = ws
 
 
 def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, resid=None, act_out=None):
@@ -120,8 +100,6 @@ def linear_fwd(x2d, w, bias=None, epi=L.EPI_STORE, out=None, out_dtype=None, res
         assert resid.stride(0) == out.stride(0)
     if x2d.dtype == torch.float32:
         _streamk(x2d.device)
-    elif epi == L.EPI_STORE and out.dtype == torch.bfloat16:
-        _blaslt(x2d.device)
     call("vit_linear_fwd", L.dt(x2d), L.dt(out), epi, M, N, K, ptr(x2d), x2d.stride(0), ptr(w), ptr(bias),
          ptr(out), out.stride(0), ptr(resid), ptr(act_out), _s(x2d))
     return (out, act_out) if epi in (L.EPI_BIAS_GELU, L.EPI_BIAS_QGELU) else out
@@ -150,8 +128,6 @@ def linear_dgrad(dy2d, w, out_dtype=torch.float32, epi=L.EPI_STORE, pre=None, ou
                 else workspace("dgrad_bias", nfl * 4, dy2d.device))
     if dy2d.dtype == torch.float32:
         _streamk(dy2d.device)
-    elif epi == L.EPI_STORE and out.dtype == torch.bfloat16 and dbias is None:
-        _blaslt(dy2d.device)
     call("vit_linear_dgrad", L.dt(dy2d), L.dt(out), epi, M, N, K, ptr(dy2d), dy2d.stride(0), ptr(w), ptr(out),
          out.stride(0), ptr(pre), ptr(dbias), ptr(part), nfl, int(defer), _s(dy2d))
     if defer:
