@@ -586,12 +586,13 @@ def test_g4_plain_gemms_bitwise_match_8wave_kernels(M, N, K):
     _close(y4, (x.double() @ w.double().t() + b.double()).float(), 8e-3, "g4 fwd vs fp64")
 
 
-@pytest.mark.parametrize("fwd_mode,dgrad_mode,wgs", [(0, 1, 0), (1, 0, 0), (0, 0, 7), (0, 0, 1), (1, 1, 0)])
+@pytest.mark.parametrize("fwd_mode,dgrad_mode,wgs,tpw", [(0, 1, 0, 1), (0, 1, 0, 0), (1, 0, 0, 0), (0, 0, 7, 0),
+                                                    (0, 0, 1, 0), (1, 1, 0, 0), (0, 0, 0, 2)])
 @pytest.mark.parametrize("M,N,K", [(1, 64, 64), (257, 136, 192), (197 * 3, 640, 448), (2000, 1088, 64),
                                    (513, 256, 3072), (300, 8, 128)])
-def test_g4_tile_walks_and_ragged_shapes(fwd_mode, dgrad_mode, wgs, M, N, K):
+def test_g4_tile_walks_and_ragged_shapes(fwd_mode, dgrad_mode, wgs, tpw, M, N, K):
     """Every tile walk (stride over G persistent workgroups, G = CUs / 7 / 1 -- one workgroup running every
-    tile in sequence -- and the row-band walk) on ragged shapes: M = 1 and 257 (a 1-row last tile), output
+    tile in sequence -- or ceil(tiles / tpw) workgroups of at most 1 / 2 tiles, and the row-band walk) on ragged shapes: M = 1 and 257 (a 1-row last tile), output
     widths 8 / 136 / 448 / 1088 (partial 8-column chunks of the last column tile), a single k-step (K = 64)
     and long reductions; the stage stream crosses tile boundaries with 1..48 k-steps per tile.  The forward
     runs on g4 whenever K % 64 == 0 and N % 8 == 0, the input gradient (reduction N) when N % 64 == 0;
@@ -603,13 +604,13 @@ def test_g4_tile_walks_and_ragged_shapes(fwd_mode, dgrad_mode, wgs, M, N, K):
     w = (_rnd(N, K, seed=N + K) * 0.05).to(bf).to(DEV)
     b = _rnd(N, seed=8).to(DEV)
     fwd_g4, dgrad_g4 = K % 64 == 0 and N % 8 == 0, N % 64 == 0 and K % 8 == 0
-    lib.vit_gemm_g4_config(fwd_mode, dgrad_mode, wgs)
+    lib.vit_gemm_g4_config(fwd_mode, dgrad_mode, wgs, tpw)
     try:
         lib.vit_gemm_g4_count(1)
         y4, d4 = _g4_pair(x, w, b, dy)
         assert lib.vit_gemm_g4_count(1) == int(fwd_g4) + int(dgrad_g4)
     finally:
-        lib.vit_gemm_g4_config(0, 1, 0)
+        lib.vit_gemm_g4_config(0, 1, 0, 1)
     y5, _ = _g4_pair(x, w, b, dy, variant=5)
     _, d1 = _g4_pair(x, w, b, dy, variant=1)
     if fwd_g4:

@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--walks", action="store_true")
     ap.add_argument("--shapes", default="")
+    ap.add_argument("--wt", action="store_true", help="also time the input gradient as RC x RC on W^T")
     a = ap.parse_args()
     lib = L.lib()
     dev, bf = "cuda", torch.bfloat16
@@ -73,15 +74,21 @@ def main():
             ours = lambda: ops.linear_dgrad(dy, w, out_dtype=bf, out=dx)  # noqa: E731
             lib_fn = lambda: torch.matmul(dy, w)  # noqa: E731
             old = [1, 3]
+            if a.wt:  # the same product as a forward (RC x RC) on a transposed copy of W
+                wt = w.t().contiguous()
+                for fm in (1, 0):
+                    lib.vit_gemm_g4_config(fm, -1, -1, -1)
+                    rec[f"g4_wt_walk{fm}"] = round(flop / timeit(lambda: ops.linear_fwd(dy, wt, None, out=dx), a.reps) / 1e12, 1)
+                lib.vit_gemm_g4_config(0, 1, 0, 1)
         walks = [(0, 1, 0)]
         if a.walks:
             walks = [(0, 1, 0), (1, 1, 0), (0, 0, 0)] if kind == "fwd" else [(0, 1, 0), (0, 0, 0)]
         for _ in range(a.rounds):
             for wk in walks:
-                lib.vit_gemm_g4_config(*wk)
+                lib.vit_gemm_g4_config(*wk, -1)
                 key = "g4" if wk == (0, 1, 0) else f"g4_walk{wk[0] if kind == 'fwd' else wk[1]}"
                 rec.setdefault(key, []).append(round(flop / timeit(ours, a.reps) / 1e12, 1))
-            lib.vit_gemm_g4_config(0, 1, 0)
+            lib.vit_gemm_g4_config(0, 1, 0, 1)
             for v in old:
                 lib.vit_gemm_variant(v)
                 rec.setdefault(f"V{v}", []).append(round(flop / timeit(ours, a.reps) / 1e12, 1))

@@ -46,7 +46,11 @@ def classify(name: str) -> str:
     if m or "pers" in name and "gemm_kernel" in name:
         pl, ql = (int(m.group(1)), int(m.group(2))) if m else (0, 0)
         return {(0, 0): "gemm fwd", (0, 1): "gemm dgrad", (1, 1): "gemm wgrad"}.get((pl, ql), "gemm other")
-    if "Cijk_" in name:  # hipBLASLt (csrc/blaslt.hip): A = W read transposed (Alik) = forward, else dgrad
+    if "_ZN2g46kernelILi0E" in name or "g4::kernel<0," in name:  # the 4-wave plain GEMM (csrc/gemm_g4.hip, round 6)
+        return "gemm fwd"
+    if "_ZN2g46kernelILi1E" in name or "g4::kernel<1," in name:
+        return "gemm dgrad"
+    if "Cijk_" in name:  # hipBLASLt (round 5's blaslt.hip): A = W read transposed (Alik) = forward, else dgrad
         return "gemm fwd" if "Cijk_Alik" in name else "gemm dgrad" if "Cijk_Ailk" in name else "gemm other"
     if "gen9gemm_kernel" in name or "gen::gemm_kernel" in name:
         return "head (fp32 generic GEMMs)"

@@ -1852,19 +1852,10 @@ int vit_linear_wgrad_partials2(int M, int split, int Na, int Ka, const void* dYa
     return p;
   };
   const big::PPProb a = prob(dYa, lddya, Xa, ldxa, Na, Ka, slabs_a), b = prob(dYb, lddyb, Xb, ldxb, Nb, Kb, slabs_b);
-  // the weight-gradient kernel pick_variant chooses (11 = w4, 8 = the ping-pong kernel; VIT_GEMM_WGRAD A/B)
-  if (pick_variant(LAY_CR, LAY_CR, Na, Ka, M, split, false) == 8) {
-    using C = big::PP<4>;
-    static bool attr = false;
-    if (!attr) {
-      (void)hipFuncSetAttribute((const void*)big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
-      attr = true;
-    }
-    hipLaunchKernelGGL((big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>), dim3(a.nwg + b.nwg),
-                       dim3(C::THREADS), C::LDS, s, a, b);
-  } else {
-    using C = w4::Default;
+  // the weight-gradient kernel pick_variant chooses: 11-15 = w4 and its ring / load-placement siblings (as
+  // launch_fast maps them), anything else the ping-pong kernel (8, the default; VIT_GEMM_WGRAD A/B)
+  auto pair_w4 = [&](auto cfg_tag) {
+    using C = decltype(cfg_tag);
     static bool attr = false;
     if (!attr) {
       (void)hipFuncSetAttribute((const void*)w4::kernel2<C, LAY_CR, LAY_CR, EPI_STORE, float, bf16>,
@@ -1873,6 +1864,24 @@ int vit_linear_wgrad_partials2(int M, int split, int Na, int Ka, const void* dYa
     }
     hipLaunchKernelGGL((w4::kernel2<C, LAY_CR, LAY_CR, EPI_STORE, float, bf16>), dim3(a.nwg + b.nwg),
                        dim3(C::THREADS), C::LDS, s, a, b);
+  };
+  switch (pick_variant(LAY_CR, LAY_CR, Na, Ka, M, split, false)) {
+    case 11: pair_w4(w4::Default{}); break;
+    case 12: pair_w4(w4::Cfg<4, 0>{}); break;
+    case 13: pair_w4(w4::Cfg<4, 2>{}); break;
+    case 14: pair_w4(w4::Cfg<3, 1>{}); break;
+    case 15: pair_w4(w4::Cfg<5, 1>{}); break;
+    default: {
+      using C = big::PP<4>;
+      static bool attr = false;
+      if (!attr) {
+        (void)hipFuncSetAttribute((const void*)big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS);
+        attr = true;
+      }
+      hipLaunchKernelGGL((big::pp_kernel2<4, LAY_CR, LAY_CR, EPI_STORE, float, bf16>), dim3(a.nwg + b.nwg),
+                         dim3(C::THREADS), C::LDS, s, a, b);
+    }
   }
   VIT_CHECK_LAUNCH();
   return 0;

@@ -30,8 +30,8 @@
 //
 // Inline asm (MFMA, fragment reads) is invisible to the compiler's waitcnt pass and hazard recognizer
 // (gemm_w4.inc has the rules): fragment destinations are named "+v" after the wait that covers them,
-// accumulators "+a" after zeroing (s_nop 4 before the first MFMA), three s_nop 7 separate the last
-// MFMA from the epilogue's accumulator reads.  Nothing in the k-step body is conditional: past the
+// accumulators are started by SrcC = 0 MFMAs in each tile's first k-step, three s_nop 7 separate the
+// last MFMA from the epilogue's accumulator reads.  Nothing in the k-step body is conditional: past the
 // stream's end the loader re-issues valid addresses into the slot nothing reads any more (and the
 // workgroup waits for them before it exits).
 // ----------------------------------------------------------------------------
@@ -41,17 +41,43 @@
 
 namespace g4 {
 
-constexpr int BK = 64, PIMG = 256 * BK * 2, STAGE = 2 * PIMG, LDS = 2 * STAGE, THREADS = 256;
-static_assert(LDS <= 163840, "LDS");
+constexpr int BK = 64, PIMG = 256 * BK * 2, THREADS = 256;  // PIMG: one operand's 256 x 64 stage image
 
 __device__ __forceinline__ void mfma_acc(f32x4& c, const bf16x8& a, const bf16x8& b) {
   asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(c) : "v"(a), "v"(b));
+}
+// a tile's first MFMA per accumulator: SrcC = inline 0 (no accumulator zeroing pass)
+__device__ __forceinline__ void mfma_zero(f32x4& c, const bf16x8& a, const bf16x8& b) {
+  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(c) : "v"(a), "v"(b));
+}
+
+// The k-step schedule (MFMA slots, kernel comment): Y fragment reads after MFMA Y0 + YS * f (f = 0..15);
+// s_waitcnt lgkmcnt(0) + barrier before MFMA B1; LDS-DMA piece u after MFMA P0 + PS * u (u = 0..15); the
+// counted vmcnt + barrier before MFMA B2, then the X reads after MFMA X0 + XS * f.  Sched<0> is the product's;
+// the others are stamped-instance alternatives (tools/g4_stamps.py --sched).
+template <int V> struct Sched;
+// PF: the 8 P pieces (the streamed activation / output-gradient rows) go out first, then the 8 Q pieces (the
+// weights, L2-resident); otherwise they alternate.
+// DP: LDS slots of the P operand (2, or 3: stage g + 3's P pieces go out in k-step g, two k-steps of slack for
+// the HBM-streamed operand; the Q ring stays 2 deep).
+// Measured (tools/g4_stamps.py, k-step cycles; profiles/r06): Sched 1 / 2 (spread or dense reads / pieces)
+// slower than 0 on every shape; PF (3) -4..-7 % on the fc1 input gradient, equal elsewhere.
+template <> struct Sched<0> { static constexpr int Y0 = 0, YS = 1, B1 = 24, P0 = 26, PS = 6, B2 = 96, X0 = 96, XS = 1, DP = 2; static constexpr bool PF = true; };
+template <> struct Sched<1> { static constexpr int Y0 = 0, YS = 2, B1 = 36, P0 = 38, PS = 5, B2 = 88, X0 = 88, XS = 2, DP = 2; static constexpr bool PF = false; };
+template <> struct Sched<2> { static constexpr int Y0 = 0, YS = 1, B1 = 20, P0 = 21, PS = 4, B2 = 96, X0 = 96, XS = 1, DP = 2; static constexpr bool PF = false; };
+template <> struct Sched<3> { static constexpr int Y0 = 0, YS = 1, B1 = 24, P0 = 26, PS = 6, B2 = 96, X0 = 96, XS = 1, DP = 2; static constexpr bool PF = false; };
+template <> struct Sched<4> { static constexpr int Y0 = 0, YS = 1, B1 = 24, P0 = 26, PS = 6, B2 = 96, X0 = 96, XS = 1, DP = 3; static constexpr bool PF = true; };
+template <class S> constexpr int pieces_before_b2() {
+  int n = 0;
+  for (int u = 0; u < 16; ++u) n += (S::P0 + S::PS * u < S::B2) ? 1 : 0;
+  return n;
 }
 
 // a workgroup's output tiles: mode 0 strides over the row-major (or group_m-banded) tile order by the
 // grid size G, mode 1 gives workgroup w row tile w and walks its column tiles
 struct Walk {
   int tiles_i, tiles_j, mode, G, group_m;
+  int epi;  // 1: every tile takes the fragment epilogue (A/B of the last tile's LDS-staged one)
 };
 __device__ __forceinline__ bool tile_at(const Walk& s, int w, int q, int& i0, int& j0) {
   int ti, tj;
@@ -74,59 +100,124 @@ __host__ __device__ __forceinline__ int tiles_of(const Walk& s, int w) {
   return w < t ? (t - w + s.G - 1) / s.G : 0;
 }
 
+// the last tile's epilogue stages bf16(acc + bias) through a [256][PITCH] LDS image (16-B row pad: a
+// fragment write's 16 rows hit distinct banks) and stores it row-contiguously
+constexpr int PITCH = 256 * 2 + 16, EPI_LDS = 256 * PITCH, RING_LDS = 5 * PIMG;  // P 3 deep + Q 2 deep at most
+constexpr int KERNEL_LDS = EPI_LDS > RING_LDS ? EPI_LDS : RING_LDS;
+static_assert(KERNEL_LDS <= 163840, "LDS");
+constexpr int NST = 32;  // epilogue store instructions per thread (either form), issued unconditionally
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
 // P RC [M x R] (forward X / input-gradient dY), Q RC [N x R] (forward W) or CR [R x N] (input-gradient
-// W read with a k stride); C bf16 [M x N] = P Q^T (+ f32 bias), R % 64 == 0, N % 8 == 0.
-template <int QL>
+// W read with a k stride); C bf16 [M x N] = P Q^T (+ f32 bias), R % 64 == 0, N % 8 == 0, M * ldc * 2 < 2^31.
+//
+// Epilogues: a tile that is not the workgroup's last stores straight from the fragments (permlane16_swap
+// pairs, 16 B per lane) while the next tile's first two stages are already loading; the last tile (every
+// tile of a one-tile workgroup) stages through LDS (the stage slots are free then) and stores 512-B row
+// segments.  Stores go through a buffer resource over C: a lane outside [M, N) gets an offset past
+// num_records, which the hardware drops, so every thread issues exactly NST stores and the next k-step's
+// counted vmcnt can let them stay in flight.
+//
+// STAMP (diagnostic instance, vit_debug_g4_stamps; the product launches never record): thread 0 writes
+// stamps[blockIdx.x * 64 + i]: 0 / 63 s_memrealtime (100 MHz) at start / end, 1 / 62 s_memtime at start /
+// end, then s_memtime per event from slot 2 on: prologue done, every k-step's start, every epilogue's
+// start and end (up to slot 61).  SD >= 0 selects it, with timing switches SD & 7 (1 = no in-loop operand
+// loads, 2 = no in-loop barriers, 4 = no epilogue stores; results wrong, timing only) and schedule SD >> 4.
+template <int QL, int SD>
 __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P, int64_t ldp,
                                                      const bf16* __restrict__ Q, int64_t ldq, int M, int N, int R,
-                                                     Epi e, Walk s) {
+                                                     Epi e, Walk s, unsigned long long* __restrict__ stamps) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = big::xcd_remap(blockIdx.x, gridDim.x);
   const int ntiles = tiles_of(s, w);
   if (ntiles <= 0) return;
   const int tid = threadIdx.x, lane = tid & 63;
+  constexpr bool STAMP = SD >= 0;
+  constexpr int dbg = SD < 0 ? 0 : (SD & 7);  // compile-time: the switches cost the timed instance nothing
+  using SC = Sched<SD < 0 ? 0 : (SD >> 4)>;
+  constexpr int NB2 = pieces_before_b2<SC>();
+  int ev = 2;
+  auto stamp = [&]() {
+    if constexpr (STAMP) {
+      if (tid == 0 && ev < 62) stamps[(int64_t)blockIdx.x * 64 + ev] = __builtin_amdgcn_s_memtime();
+      ++ev;
+    }
+  };
+  if constexpr (STAMP) {
+    if (tid == 0) {
+      stamps[(int64_t)blockIdx.x * 64 + 0] = __builtin_amdgcn_s_memrealtime();
+      stamps[(int64_t)blockIdx.x * 64 + 1] = __builtin_amdgcn_s_memtime();
+    }
+  }
+  auto barrier = [&]() {
+    if constexpr (!(dbg & 2)) big::lds_barrier();
+  };
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = wave >> 1, wj = wave & 1;
   const int nk = R / BK;
 
-  // ---- loader: the tile and k-step of the next stage to issue, and its per-lane source offsets
-  int qL = 0, kL = 0, i0L = 0, j0L = 0;
-  tile_at(s, w, 0, i0L, j0L);
+  // ---- loaders: P and Q each keep the tile and k-step of the next stage they issue (P runs DP - 2 stages
+  // ahead of Q) and that tile's per-lane source offsets.  LDS: DP = 2: two [P | Q] stage slots (the P
+  // and Q images of a stage adjacent: 4 % fewer cycles per k-step on the forward than separate rings,
+  // profiles/r06); DP = 3: P slots [0, 3) x PIMG, then the two Q slots.
+  constexpr int DP = SC::DP;
+  constexpr int PSTR = DP == 2 ? 2 * PIMG : PIMG, QOFF = DP == 2 ? PIMG : DP * PIMG, QSTR = DP == 2 ? 2 * PIMG : PIMG;
+  char* const qring = smem + QOFF;
+  int qP = 0, kP = 0, i0P = 0, jP = 0, qQ = 0, kQ = 0, iQ = 0, j0Q = 0;
+  tile_at(s, w, 0, i0P, jP);
+  tile_at(s, w, 0, iQ, j0Q);
   uint32_t offP[8], offQ[8];
-  auto set_offsets = [&]() {
+  // live = false (past the stream's end): every lane re-reads the operand's first 16 B (in L2) into a slot
+  // nothing reads any more, so the k-step body issues its 16 pieces unconditionally (one code path, exact
+  // vmcnt counts)
+  auto set_p = [&](bool live) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int row = (wave * 8 + u) * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ big::rc_sw<64>(row);
+      const uint32_t op = (uint32_t)((int64_t)min(i0P + row, M - 1) * ldp * 2 + c * 16);
+      offP[u] = live ? op : 0u;
+    }
+  };
+  auto set_q = [&](bool live) {
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int t = wave * 8 + u;
-      const int row = t * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ big::rc_sw<64>(row);
-      offP[u] = (uint32_t)((int64_t)min(i0L + row, M - 1) * ldp * 2 + c * 16);
-      if constexpr (QL == LAY_RC)
-        offQ[u] = (uint32_t)((int64_t)min(j0L + row, N - 1) * ldq * 2 + c * 16);
-      else
-        offQ[u] = (uint32_t)(big::crh_src<256>(t, lane, ldq, j0L, N) * 2);
+      uint32_t oq;
+      if constexpr (QL == LAY_RC) {
+        const int row = t * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ big::rc_sw<64>(row);
+        oq = (uint32_t)((int64_t)min(j0Q + row, N - 1) * ldq * 2 + c * 16);
+      } else {
+        oq = (uint32_t)(big::crh_src<256>(t, lane, ldq, j0Q, N) * 2);
+      }
+      offQ[u] = live ? oq : 0u;
     }
   };
-  set_offsets();
+  set_p(true);
+  set_q(true);
   const int64_t qstep = QL == LAY_RC ? (int64_t)BK * 2 : (int64_t)BK * ldq * 2;  // bytes per k-step
-  // piece u (0..15) of the loader's stage (operand bases pb / qb at its k-step) into LDS slot `buf`:
-  // even u = P piece u / 2, odd u = Q piece u / 2
-  auto piece = [&](int u, const char* pb, const char* qb, char* buf) {
-    if ((u & 1) == 0)
-      __builtin_amdgcn_global_load_lds((const void*)(pb + offP[u >> 1]), LDS_PTR(buf + (wave * 8 + (u >> 1)) * 1024),
-                                       16, 0, 0);
-    else
-      __builtin_amdgcn_global_load_lds((const void*)(qb + offQ[u >> 1]),
-                                       LDS_PTR(buf + PIMG + (wave * 8 + (u >> 1)) * 1024), 16, 0, 0);
+  auto pbase = [&]() { return reinterpret_cast<const char*>(P) + (int64_t)kP * BK * 2; };
+  auto qbase = [&]() { return reinterpret_cast<const char*>(Q) + (int64_t)kQ * qstep; };
+  auto piece_p = [&](int u, const char* pb, char* buf) {
+    __builtin_amdgcn_global_load_lds((const void*)(pb + offP[u]), LDS_PTR(buf + (wave * 8 + u) * 1024), 16, 0, 0);
   };
-  auto pbase = [&]() { return reinterpret_cast<const char*>(P) + (int64_t)kL * BK * 2; };
-  auto qbase = [&]() { return reinterpret_cast<const char*>(Q) + (int64_t)kL * qstep; };
-  // past the stream's end the loader keeps re-issuing its last tile's first k-steps (valid addresses)
-  // into the slot nothing reads any more, so the k-step body has no stream-end branch
-  auto advance = [&]() {
-    if (++kL == nk) {
-      kL = 0;
-      ++qL;
-      if (tile_at(s, w, qL, i0L, j0L)) set_offsets();
+  auto piece_q = [&](int u, const char* qb, char* buf) {
+    __builtin_amdgcn_global_load_lds((const void*)(qb + offQ[u]), LDS_PTR(buf + (wave * 8 + u) * 1024), 16, 0, 0);
+  };
+  auto advance_p = [&]() {
+    if (++kP == nk) {
+      kP = 0;
+      ++qP;
+      set_p(tile_at(s, w, qP, i0P, jP));
+    }
+  };
+  auto advance_q = [&]() {
+    if (++kQ == nk) {
+      kQ = 0;
+      ++qQ;
+      set_q(tile_at(s, w, qQ, iQ, j0Q));
     }
   };
 
@@ -135,19 +226,20 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
 #pragma unroll
   for (int kk = 0; kk < 2; ++kk) {
     rc_p[kk] = (uint32_t)(wi * 128 * 128 + big::rc_off<64>(lane & 15, kk * 4 + (lane >> 4)));
-    rc_q[kk] = (uint32_t)(PIMG + wj * 128 * 128 + big::rc_off<64>(lane & 15, kk * 4 + (lane >> 4)));
+    rc_q[kk] = (uint32_t)(wj * 128 * 128 + big::rc_off<64>(lane & 15, kk * 4 + (lane >> 4)));
   }
 #pragma unroll
   for (int lh = 0; lh < 2; ++lh)
 #pragma unroll
-    for (int h = 0; h < 2; ++h) crh_q[lh][h] = PIMG + big::crh_lane<256>(lane, lh, h) + (uint32_t)(wj * 4 * 1024);
-  auto read_frag = [&](auto kkI, auto fI, uint32_t cur, bf16x8 (&pf)[8], bf16x8 (&qf)[8]) {
+    for (int h = 0; h < 2; ++h) crh_q[lh][h] = big::crh_lane<256>(lane, lh, h) + (uint32_t)(wj * 4 * 1024);
+  // cp / cq: the LDS byte addresses of the P / Q slot the fragments come from
+  auto read_frag = [&](auto kkI, auto fI, uint32_t cp, uint32_t cq, bf16x8 (&pf)[8], bf16x8 (&qf)[8]) {
     constexpr int kk = decltype(kkI)::value, f = decltype(fI)::value;
     if constexpr (f < 8) {
-      if constexpr (QL == LAY_RC) qf[f] = big::asm_read128_off<f * 2048>(cur + rc_q[kk]);
-      else qf[f] = big::frag_crh<256, kk, f>(crh_q, cur);
+      if constexpr (QL == LAY_RC) qf[f] = big::asm_read128_off<f * 2048>(cq + rc_q[kk]);
+      else qf[f] = big::frag_crh<256, kk, f>(crh_q, cq);
     } else {
-      pf[f - 8] = big::asm_read128_off<(f - 8) * 2048>(cur + rc_p[kk]);
+      pf[f - 8] = big::asm_read128_off<(f - 8) * 2048>(cp + rc_p[kk]);
     }
   };
   auto settle = [&](bf16x8 (&pf)[8], bf16x8 (&qf)[8]) {
@@ -157,105 +249,191 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  // accumulators: defined (as garbage, no instruction) here; every tile's first k-step writes them with
+  // SrcC = 0 MFMAs (mfma_zero), so no tile pays a 256-instruction zeroing pass
   f32x4 acc[8][8];
-  auto zero_acc = [&]() {
 #pragma unroll
-    for (int a = 0; a < 8; ++a)
-#pragma unroll
-      for (int b = 0; b < 8; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int a = 0; a < 8; ++a)
-      asm volatile("" : "+a"(acc[a][0]), "+a"(acc[a][1]), "+a"(acc[a][2]), "+a"(acc[a][3]), "+a"(acc[a][4]),
-                        "+a"(acc[a][5]), "+a"(acc[a][6]), "+a"(acc[a][7]));
-    asm volatile("s_nop 4" ::: "memory");  // accumulator writes (VALU) -> first MFMA's SrcC
-    __builtin_amdgcn_sched_barrier(0);
+  for (int a = 0; a < 8; ++a)
+    asm volatile("" : "=a"(acc[a][0]), "=a"(acc[a][1]), "=a"(acc[a][2]), "=a"(acc[a][3]), "=a"(acc[a][4]),
+                      "=a"(acc[a][5]), "=a"(acc[a][6]), "=a"(acc[a][7]));
+
+  // epilogue stores: C through a buffer resource, out-of-range lanes dropped by the range check
+  const __amdgpu_buffer_rsrc_t crs =
+      __builtin_amdgcn_make_buffer_rsrc(e.C, (short)0, (int)((int64_t)M * e.ldc * 2), 0x00020000);
+  auto store16 = [&](i32x4 v, int i, int col, bool ok) {
+    const int off = ok ? (int)(((int64_t)i * e.ldc + col) * 2) : (int)0x80000000;
+    if constexpr (!(dbg & 4)) __builtin_amdgcn_raw_buffer_store_b128(v, crs, off, 0, 0);
   };
 
-  // ---- prologue: stages 0 and 1 in flight, stage 0 landed and visible, X = its k-substep 0
+  // ---- prologue: P stages 0..DP-1 and Q stages 0, 1 in flight, stage 0 landed and visible, X = its k-substep 0
   bf16x8 pX[8], qX[8], pY[8], qY[8];
-  for (int st = 0; st < 2; ++st) {
-    const char *pb = pbase(), *qb = qbase();
+  auto issue_p = [&](char* buf) {
+    const char* pb = pbase();
 #pragma unroll
-    for (int u = 0; u < 16; ++u) piece(u, pb, qb, smem + st * STAGE);
-    advance();
+    for (int u = 0; u < 8; ++u) piece_p(u, pb, buf);
+    advance_p();
+  };
+  auto issue_q = [&](char* buf) {
+    const char* qb = qbase();
+#pragma unroll
+    for (int u = 0; u < 8; ++u) piece_q(u, qb, buf);
+    advance_q();
+  };
+  issue_p(smem);
+  issue_q(qring);
+  issue_p(smem + PSTR);  // stage 1 (or, on a one-stage stream, the stream-end re-read into a free slot)
+  issue_q(qring + QSTR);
+  if constexpr (DP == 3) {
+    issue_p(smem + 2 * PSTR);
+    big::wait_vm<24>();
+  } else {
+    big::wait_vm<16>();
   }
-  big::wait_vm<16>();
   big::lds_barrier();
   {
-    const uint32_t cur = big::lds_addr(smem);
-    big::Unroll<16>::run([&](auto fI) { read_frag(std::integral_constant<int, 0>{}, fI, cur, pX, qX); });
+    const uint32_t cp = big::lds_addr(smem), cq = big::lds_addr(qring);
+    big::Unroll<16>::run([&](auto fI) { read_frag(std::integral_constant<int, 0>{}, fI, cp, cq, pX, qX); });
     settle(pX, qX);
   }
-  zero_acc();
+  stamp();
 
-  int g = 0;
+  int g = 0, gp = 0;  // stage index and its P slot (g % DP)
   int i0 = 0, j0 = 0;
   for (int q = 0; q < ntiles; ++q) {
     tile_at(s, w, q, i0, j0);
-    for (int k = 0; k < nk; ++k, ++g) {
+    // one k-step of stage g (FIRST: the tile's first; it is peeled off the loop below, so the steady-state
+    // loop is one code path whose fragment registers need no copies at its back edge)
+    auto step = [&](auto firstI, bool stores) {
+      stamp();
       const char *pb = pbase(), *qb = qbase();
-      char* slot = smem + (g & 1) * STAGE;
-      const uint32_t cur = big::lds_addr(smem + (g & 1) * STAGE);
-      const uint32_t nxt = big::lds_addr(smem + ((g + 1) & 1) * STAGE);
-      big::Unroll<128>::run([&](auto mI) {
-        constexpr int m = decltype(mI)::value;
-        constexpr int a = (m % 64) / 8, b = m % 8;
-        if constexpr (m == 24) {  // every wave's reads of stage g are done: its slot takes stage g + 2
-          settle(pY, qY);
-          big::lds_barrier();
-        }
-        if constexpr (m == 96) {  // stage g + 1 landed (this wave's pieces) and visible (barrier)
-          big::wait_vm<12>();
-          big::lds_barrier();
-        }
-        if constexpr (m < 64) mfma_acc(acc[a][b], qX[b], pX[a]);
-        else mfma_acc(acc[a][b], qY[b], pY[a]);
-        if constexpr (m < 16) read_frag(std::integral_constant<int, 1>{}, std::integral_constant<int, m>{}, cur, pY, qY);
-        if constexpr (m >= 96 && m < 112)
-          read_frag(std::integral_constant<int, 0>{}, std::integral_constant<int, m - 96>{}, nxt, pX, qX);
-        if constexpr (m >= 26 && (m - 26) % 6 == 0 && (m - 26) / 6 < 16) {
-          piece((m - 26) / 6, pb, qb, slot);
-          if constexpr ((m - 26) / 6 == 15) advance();
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      });
-      settle(pX, qX);
-    }
+      // this k-step reads P slot gp = g % DP and Q slot g % 2; stage g + DP's P pieces and stage g + 2's Q
+      // pieces go into those slots after the first barrier, stage g + 1 comes from the next ones
+      const int gp1 = gp + 1 == DP ? 0 : gp + 1;
+      char* const pslot = smem + gp * PSTR;
+      char* const qslot = qring + (g & 1) * QSTR;
+      const uint32_t cp = big::lds_addr(pslot), cq = big::lds_addr(qslot);
+      const uint32_t np = big::lds_addr(smem + gp1 * PSTR), nq = big::lds_addr(qring + ((g + 1) & 1) * QSTR);
+      // one k-step; FIRST: the tile's first (its k-substep-0 MFMAs start the accumulators from 0)
+      auto kstep = [&](auto firstI) {
+        constexpr bool FIRST = decltype(firstI)::value;
+        big::Unroll<128>::run([&](auto mI) {
+          constexpr int m = decltype(mI)::value;
+          constexpr int a = (m % 64) / 8, b = m % 8;
+          if constexpr (m == SC::B1) {  // every wave's reads of stage g are done: its slot takes stage g + 2
+            settle(pY, qY);
+            barrier();
+          }
+          if constexpr (m == SC::B2) {  // stage g + 1 landed (this wave's pieces; counted) and visible (barrier)
+            if (FIRST && stores) big::wait_vm<NB2 + NST>();  // the stores went out after stage g + 1's pieces
+            else big::wait_vm<NB2>();
+            barrier();
+          }
+          if constexpr (m < 64 && FIRST) mfma_zero(acc[a][b], qX[b], pX[a]);
+          else if constexpr (m < 64) mfma_acc(acc[a][b], qX[b], pX[a]);
+          else mfma_acc(acc[a][b], qY[b], pY[a]);
+          if constexpr (m >= SC::Y0 && (m - SC::Y0) % SC::YS == 0 && (m - SC::Y0) / SC::YS < 16)
+            read_frag(std::integral_constant<int, 1>{}, std::integral_constant<int, (m - SC::Y0) / SC::YS>{}, cp, cq, pY, qY);
+          if constexpr (m >= SC::X0 && (m - SC::X0) % SC::XS == 0 && (m - SC::X0) / SC::XS < 16)
+            read_frag(std::integral_constant<int, 0>{}, std::integral_constant<int, (m - SC::X0) / SC::XS>{}, np, nq, pX, qX);
+          if constexpr (m >= SC::P0 && (m - SC::P0) % SC::PS == 0 && (m - SC::P0) / SC::PS < 16) {
+            constexpr int u = (m - SC::P0) / SC::PS;
+            constexpr int v = SC::PF ? u : (u & 1) * 8 + (u >> 1);  // 0..7 P pieces, 8..15 Q pieces
+            if constexpr (!(dbg & 1)) {
+              if constexpr (v < 8) piece_p(v, pb, pslot);
+              else piece_q(v - 8, qb, qslot);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        settle(pX, qX);  // inside each instance: no fragment is live-in to the join with a read in flight
+      };
+      kstep(firstI);
+      advance_p();  // the loaders move to stages g + DP + 1 and g + 3 (issued in the next k-step)
+      advance_q();
+      gp = gp1;
+      ++g;
+    };
+    step(std::true_type{}, q > 0);  // q > 0: the previous tile's NST fragment-epilogue stores are in flight
+    for (int k = 1; k < nk; ++k) step(std::false_type{}, false);
     // ---- epilogue of tile q: acc[a][b] holds C[i][j..j+3], i = i0 + wi*128 + 16a + lane%16,
-    // j = j0 + wj*128 + 16b + 4*(lane/16); fragment pairs widened to 16-B stores (permlane16_swap)
+    // j = j0 + wj*128 + 16b + 4*(lane/16)
     asm volatile("s_nop 7\n s_nop 7\n s_nop 7" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
+    stamp();
     const int gq = lane >> 4;
-    const int colsel = (gq & 1) * 16 + (gq >> 1) * 8;
     f32x4 bias4[8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const int j = j0 + wj * 128 + b * 16 + 4 * gq;
       bias4[b] = (e.bias && j < N) ? *reinterpret_cast<const f32x4*>(e.bias + j) : f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    // a tile that is not the workgroup's last: fragment pairs widened to 16-B stores (permlane16_swap; lane
+    // group gq then holds 8 columns of the pair).  The last tile (staged): once the stream-end pieces have
+    // landed and every wave's reads retired (wait + barrier) the stage slots are free, so the tile goes
+    // through a bf16 LDS image and out in 512-B row segments.
+    const bool staged = !(q + 1 < ntiles || s.epi == 1);
+    if (staged) {
+      big::wait_vm<0>();
+      big::lds_barrier();
+    }
+    const int colsel = (gq & 1) * 16 + (gq >> 1) * 8;
 #pragma unroll
     for (int a = 0; a < 8; ++a) {
       asm volatile("" : "+a"(acc[a][0]), "+a"(acc[a][1]), "+a"(acc[a][2]), "+a"(acc[a][3]), "+a"(acc[a][4]),
                         "+a"(acc[a][5]), "+a"(acc[a][6]), "+a"(acc[a][7]));
-      const int i = i0 + wi * 128 + a * 16 + (lane & 15);
+      const int r = wi * 128 + a * 16 + (lane & 15), i = i0 + r;
 #pragma unroll
       for (int b = 0; b < 8; b += 2) {
-        const int jp = j0 + wj * 128 + b * 16;
-        store_pair_bf16(e.C, e.ldc, i, jp + colsel, acc[a][b] + bias4[b], acc[a][b + 1] + bias4[b + 1],
-                        i < M && jp + colsel < N);
+        const f32x4 x = acc[a][b] + bias4[b], y = acc[a][b + 1] + bias4[b + 1];
+        const bf16x4 px = {(bf16)x[0], (bf16)x[1], (bf16)x[2], (bf16)x[3]};
+        const bf16x4 py = {(bf16)y[0], (bf16)y[1], (bf16)y[2], (bf16)y[3]};
+        if (staged) {
+          char* row = smem + r * PITCH + (wj * 128 + b * 16 + 4 * gq) * 2;
+          *reinterpret_cast<bf16x4*>(row) = px;
+          *reinterpret_cast<bf16x4*>(row + 32) = py;
+        } else {
+          typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+          const u32x2 ux = __builtin_bit_cast(u32x2, px), uy = __builtin_bit_cast(u32x2, py);
+          const auto r0 = __builtin_amdgcn_permlane16_swap(ux[0], uy[0], false, false);
+          const auto r1 = __builtin_amdgcn_permlane16_swap(ux[1], uy[1], false, false);
+          const int col = j0 + wj * 128 + b * 16 + colsel;
+          store16(i32x4{(int)r0[0], (int)r1[0], (int)r0[1], (int)r1[1]}, i, col, i < M && col < N);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one accumulator row at a time
+    }
+    if (staged) {
+      big::lds_barrier();
+      const int c = tid & 31, r0 = tid >> 5;
+      const int col = j0 + c * 8;
+#pragma unroll 8
+      for (int p = 0; p < NST; ++p) {
+        const int r = r0 + 8 * p;
+        const i32x4 v = *reinterpret_cast<const i32x4*>(smem + r * PITCH + c * 16);
+        store16(v, i0 + r, col, i0 + r < M && col < N);
       }
     }
-    if (q + 1 < ntiles) zero_acc();
+    stamp();
   }
-  big::wait_vm<0>();  // the stream-end pieces land before the workgroup's LDS is released
+  if (s.epi == 1) big::wait_vm<0>();  // the stream-end pieces land before the workgroup's LDS is released
+  if constexpr (STAMP) {
+    if (tid == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stamps[(int64_t)blockIdx.x * 64 + 62] = __builtin_amdgcn_s_memtime();
+      stamps[(int64_t)blockIdx.x * 64 + 63] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 }  // namespace g4
 
 namespace {
-// VIT_GEMM_G4 (0 = off), VIT_G4_MODE_{FWD,DGRAD} (0 stride, 1 band), VIT_G4_WGS (stride-walk grid cap)
-int g_g4[4] = {-2, -2, -2, -2};
+// VIT_GEMM_G4 (0 = off), VIT_G4_MODE_{FWD,DGRAD} (0 stride, 1 band), VIT_G4_WGS (stride-walk grid cap),
+// VIT_G4_TPW (stride walk: at most this many tiles per workgroup, 0 = no limit)
+int g_g4[6] = {-2, -2, -2, -2, -2, -2};
+int g_g4_dbg = 0;  // timing switches of the stamped instance (vit_debug_g4_stamps)
 unsigned g_g4_launches = 0;  // host-side count of g4 launches (tests: the plain GEMMs took this kernel)
+unsigned long long* g_g4_stamps = nullptr;  // vit_debug_g4_stamps: launch the stamped instance
 int g4_env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
@@ -266,6 +444,9 @@ void g4_env() {
   g_g4[1] = g4_env_int("VIT_G4_MODE_FWD", 0);
   g_g4[2] = g4_env_int("VIT_G4_MODE_DGRAD", 1);
   g_g4[3] = g4_env_int("VIT_G4_WGS", 0);
+  g_g4[4] = g4_env_int("VIT_G4_TPW", 1);  // in the step one tile per workgroup measured best for the
+                                          // forward (7267 vs 7061-7091 img/s for 2, 3, 3.8 tiles / CU)
+  g_g4[5] = g4_env_int("VIT_G4_EPI", 0);
 }
 int g4_cus() {
   static int n = 0;
@@ -280,22 +461,43 @@ template <int QL>
 int launch(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, const Epi& e, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)g4::kernel<QL>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::LDS);
+    for (const void* k : {(const void*)g4::kernel<QL, -1>, (const void*)g4::kernel<QL, 0>, (const void*)g4::kernel<QL, 1>,
+                          (const void*)g4::kernel<QL, 2>, (const void*)g4::kernel<QL, 4>, (const void*)g4::kernel<QL, 16>,
+                          (const void*)g4::kernel<QL, 32>, (const void*)g4::kernel<QL, 48>, (const void*)g4::kernel<QL, 64>})
+      (void)hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, g4::KERNEL_LDS);
     attr = true;
   }
   g4::Walk w;
   w.tiles_i = (M + 255) / 256;
   w.tiles_j = (N + 255) / 256;
   w.group_m = QL == LAY_RC ? e.group_m : 0;
+  w.epi = g_g4[5];
   w.mode = g_g4[QL == LAY_RC ? 1 : 2] == 1 ? 1 : 0;
   if (w.mode == 1) {
     w.G = w.tiles_i;
   } else {
     const int tiles = w.tiles_i * w.tiles_j, cap = g_g4[3] > 0 ? g_g4[3] : g4_cus();
     w.G = tiles < cap ? tiles : cap;
+    if (g_g4[4] > 0 && w.G < (tiles + g_g4[4] - 1) / g_g4[4]) w.G = (tiles + g_g4[4] - 1) / g_g4[4];
   }
-  hipLaunchKernelGGL((g4::kernel<QL>), dim3(w.G), dim3(g4::THREADS), g4::LDS, s, (const bf16*)P, ldp,
-                     (const bf16*)Q, ldq, M, N, R, e, w);
+  auto go = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(w.G), dim3(g4::THREADS), g4::KERNEL_LDS, s, (const bf16*)P, ldp, (const bf16*)Q, ldq,
+                       M, N, R, e, w, g_g4_stamps);
+  };
+  if (!g_g4_stamps) {
+    go(g4::kernel<QL, -1>);
+  } else {
+    switch (g_g4_dbg) {  // the stamped instances built: schedules 0-3, and schedule 0 with each timing switch
+      case 1: go(g4::kernel<QL, 1>); break;
+      case 2: go(g4::kernel<QL, 2>); break;
+      case 4: go(g4::kernel<QL, 4>); break;
+      case 16: go(g4::kernel<QL, 16>); break;
+      case 32: go(g4::kernel<QL, 32>); break;
+      case 48: go(g4::kernel<QL, 48>); break;
+      case 64: go(g4::kernel<QL, 64>); break;
+      default: go(g4::kernel<QL, 0>); break;
+    }
+  }
   ++g_g4_launches;
   return (int)hipGetLastError();
 }
@@ -312,6 +514,7 @@ int g4_launch(int q_layout, const void* P, int64_t ldp, const void* Q, int64_t l
               const Epi& e, hipStream_t s) {
   g4_env();
   if (split > 1 || R <= 0 || R % g4::BK || N < 8 || N % 8 || e.csum || e.slab || M <= 0) return -1;
+  if ((int64_t)M * e.ldc * 2 >= ((int64_t)1 << 31) || e.ldc % 8) return -1;  // buffer-store offsets are int32
   return q_layout == LAY_RC ? launch<LAY_RC>(P, ldp, Q, ldq, M, N, R, e, s)
                             : launch<LAY_CR>(P, ldp, Q, ldq, M, N, R, e, s);
 }
@@ -319,12 +522,23 @@ int g4_launch(int q_layout, const void* P, int64_t ldp, const void* Q, int64_t l
 extern "C" {
 
 // Tuning / test hook: tile walk of the forward and input-gradient classes (0 = stride, 1 = row band, -1 =
-// keep) and the stride walk's workgroup cap (0 = the CU count, -1 = keep).  Returns 0.
-int vit_gemm_g4_config(int fwd_mode, int dgrad_mode, int wgs) {
+// keep), the stride walk's workgroup cap (0 = the CU count, -1 = keep) and its tiles per workgroup (the
+// grid grows to ceil(tiles / tpw) workgroups; 0 = no limit, -1 = keep).  Returns 0.
+int vit_gemm_g4_config(int fwd_mode, int dgrad_mode, int wgs, int tpw) {
   g4_env();
   if (fwd_mode >= 0) g_g4[1] = fwd_mode;
   if (dgrad_mode >= 0) g_g4[2] = dgrad_mode;
   if (wgs >= 0) g_g4[3] = wgs;
+  if (tpw >= 0) g_g4[4] = tpw;
+  return 0;
+}
+
+// Diagnostic (not in the header): while buf != NULL every g4 launch runs the stamped instance, writing
+// 64 stamps per workgroup into buf (>= grid * 64 * 8 bytes; see g4::kernel); dbg = timing switches | 16 *
+// schedule (the instances built: 0, 1, 2, 4, 16, 32, 48, 64).
+int vit_debug_g4_stamps(void* buf, int dbg) {
+  g_g4_stamps = (unsigned long long*)buf;
+  g_g4_dbg = dbg;
   return 0;
 }
 

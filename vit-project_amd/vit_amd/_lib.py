@@ -27,7 +27,7 @@ SIGNATURES = {
     "vit_abi_version": [],
     "vit_gemm_variant": [i32],
     "vit_gemm_group": [i32, i32],
-    "vit_gemm_g4_config": [i32, i32, i32],
+    "vit_gemm_g4_config": [i32, i32, i32, i32],
     "vit_gemm_g4_count": [i32],
     "vit_gemm_streamk_workspace": [vp, vp, i64, vp, i32],
     "vit_gemm_rc_chunk_rows": [i32, i64],
