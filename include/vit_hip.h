@@ -69,6 +69,12 @@ int vit_gemm_g4_config(int fwd_mode, int dgrad_mode, int wgs, int tpw);
 /* Host-side count of g4 launches since the last reset (reset != 0 zeroes it); no GPU call. */
 int vit_gemm_g4_count(int reset);
 
+/* Tuning / test hook: the fc2 GELU' input gradient (vit_linear_dgrad with EPI_GELU_BWD / EPI_QGELU_BWD, bf16)
+ * on g4 (1: the act' tile arrives by LDS-DMA in the two stage slots past the stream's end, products in place,
+ * column partials for the fc1 bias gradient) or on the 8-wave V1 kernel (0); -1 keeps.  Returns the previous
+ * setting (default VIT_G4_GELU, else 0). */
+int vit_gemm_g4_gelu(int on);
+
 /* Stream-K workspace for the fp32 MFMA GEMMs launched on `stream` (the reference-precision C3 path,
  * NEWP:274): part >= 4 * CUs * 128*128 floats, counters >= 2 * CUs ints, zero-filled before first use
  * (kernels leave them zero).  With it, an f32 GEMM whose tile count would leave a ragged last round

@@ -621,6 +621,48 @@ def test_g4_tile_walks_and_ragged_shapes(fwd_mode, dgrad_mode, wgs, tpw, M, N, K
     _close(d4, (dy.double() @ w.double()).float(), 8e-3, "g4 dgrad vs fp64")
 
 
+def _gelu_dgrad(dy, w, pre, variant=-1, g4=1):
+    """The GELU' input gradient dy @ w * pre with its fused column sums (the fc1 bias gradient), GEMM
+    variant `variant` forced (-1 = default) and the g4 form on / off."""
+    lib = L.lib()
+    prev = lib.vit_gemm_g4_gelu(g4)
+    lib.vit_gemm_variant(variant)
+    try:
+        db = torch.empty(w.shape[1], device=DEV)
+        out = ops.linear_dgrad(dy, w, out_dtype=torch.bfloat16, epi=L.EPI_GELU_BWD, pre=pre, dbias=db)
+        torch.cuda.synchronize()
+    finally:
+        lib.vit_gemm_variant(-1)
+        lib.vit_gemm_g4_gelu(prev)
+    return out, db
+
+
+@pytest.mark.parametrize("M,K,N", [(50432, 3072, 768), (1000, 3072, 768), (257, 136, 128), (333, 1088, 192),
+                                   (1, 64, 128), (2000, 512, 64)])
+def test_g4_gelu_dgrad_matches_v1(M, K, N):
+    """The fc2 GELU' input gradient (C = dY W * act', VIT r04 item 3's fused epilogue) on g4 (vit_gemm_g4_gelu:
+    the act' tile arrives by LDS-DMA in the two stage slots past the stream's end, the products replace it in
+    the LDS image) against the 8-wave V1 kernel forced: the step shape (M = 50432, 3072 columns, reduction
+    768), ragged rows / columns and the 2- and 3-k-step reductions.  C agrees BIT FOR BIT (same k order, same
+    f32 product, same rounding); the fused column sums (fc1's bias gradient) add the same f32 products in
+    another order (V1: its staged rows; g4: a lane's 4 rows, then the 16-lane butterfly), so they are held to
+    1e-5 relative of V1 and to fp64.  A one-k-step reduction (N = 64) is not taken by g4 (launch count 0)."""
+    lib = L.lib()
+    bf = torch.bfloat16
+    dy = _rnd(M, N, seed=M + N + 11).to(bf).to(DEV)
+    w = (_rnd(N, K, seed=N * K + 3) * 0.05).to(bf).to(DEV)
+    pre = (_rnd(M, K, seed=M + K + 5).abs() * 0.6).to(bf).to(DEV)
+    lib.vit_gemm_g4_count(1)
+    c4, db4 = _gelu_dgrad(dy, w, pre)
+    assert lib.vit_gemm_g4_count(1) == (1 if N >= 128 else 0)
+    c1, db1 = _gelu_dgrad(dy, w, pre, variant=1, g4=0)
+    assert torch.equal(c4, c1), "g4 GELU' input gradient differs from V1"
+    ref = (dy.double() @ w.double()) * pre.double()
+    _close(c4, ref.float(), 8e-3, "g4 GELU' dgrad vs fp64")
+    assert torch.allclose(db4, db1, rtol=1e-5, atol=1e-5 * float(db1.abs().max()) + 1e-30), "column sums vs V1"
+    _close(db4, ref.sum(0).float(), 1e-4, "fused column sums vs fp64")
+
+
 # ---------------------------------------------------------------------------- LayerNorm
 
 @pytest.mark.parametrize("D", [768, 1024, 64, 200])

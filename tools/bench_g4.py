@@ -39,7 +39,10 @@ def main():
     ap.add_argument("--walks", action="store_true")
     ap.add_argument("--shapes", default="")
     ap.add_argument("--wt", action="store_true", help="also time the input gradient as RC x RC on W^T")
+    ap.add_argument("--gelu", action="store_true", help="only the fc2 GELU' input gradient: g4 vs V1")
     a = ap.parse_args()
+    if a.gelu:
+        return gelu(a)
     lib = L.lib()
     dev, bf = "cuda", torch.bfloat16
     torch.backends.cuda.preferred_blas_library("hipblaslt")
@@ -95,6 +98,27 @@ def main():
                 lib.vit_gemm_variant(-1)
             rec.setdefault("hipblaslt", []).append(round(flop / timeit(lib_fn, a.reps) / 1e12, 1))
         print(json.dumps(rec), flush=True)
+
+
+def gelu(a):
+    lib = L.lib()
+    dev, bf = "cuda", torch.bfloat16
+    M, K, N = 256 * 197, 3072, 768  # dx [M, 3072] = dy [M, 768] @ W2 [768, 3072] * act'
+    g = torch.Generator(device=dev).manual_seed(5)
+    dy = torch.randn(M, N, device=dev, generator=g).to(bf)
+    w = (torch.randn(N, K, device=dev, generator=g) * 0.05).to(bf)
+    pre = torch.rand(M, K, device=dev, generator=g).to(bf)
+    out = torch.empty(M, K, device=dev, dtype=bf)
+    db = torch.empty(K, device=dev)
+    flop = 2.0 * M * N * K
+    fn = lambda: ops.linear_dgrad(dy, w, out_dtype=bf, epi=L.EPI_GELU_BWD, pre=pre, dbias=db, out=out)  # noqa: E731
+    rec = {"class": "gelu_dgrad", "M": M, "N": K, "K": N}
+    for _ in range(a.rounds):
+        for tag, on in (("g4", 1), ("V1", 0)):
+            prev = lib.vit_gemm_g4_gelu(on)
+            rec.setdefault(tag, []).append(round(flop / timeit(fn, a.reps) / 1e12, 1))
+            lib.vit_gemm_g4_gelu(prev)
+    print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

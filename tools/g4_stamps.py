@@ -67,7 +67,8 @@ def main():
     D, Fh, B = 768, 3072, 256
     m0 = (B // 2 + 3 * B // 64) * 197
     cases = [("fwd", "qkv", m0, 3 * D, D), ("fwd", "proj", m0, D, D), ("fwd", "fc2", m0, D, Fh),
-             ("dgrad", "qkv", B * 197, 3 * D, D), ("dgrad", "fc1", B * 197, Fh, D), ("dgrad", "proj", B * 197, D, D)]
+             ("dgrad", "qkv", B * 197, 3 * D, D), ("dgrad", "fc1", B * 197, Fh, D), ("dgrad", "proj", B * 197, D, D),
+             ("gelu", "fc2", B * 197, D, Fh)]  # gelu: the fc2 GELU' input gradient with its column sums
     if a.shapes:
         keep = set(a.shapes.split(","))
         cases = [c for c in cases if f"{c[0]}_{c[1]}" in keep]
@@ -84,7 +85,12 @@ def main():
             nk, tiles = K // 64, ((M + 255) // 256) * (N // 256)
         else:
             dy = torch.randn(M, N, device=dev, generator=g).to(bf)
-            run = lambda: ops.linear_dgrad(dy, w, out_dtype=bf)  # noqa: E731
+            if kind == "gelu":
+                pre = torch.rand(M, K, device=dev, generator=g).to(bf)
+                db = torch.empty(K, device=dev)
+                run = lambda: ops.linear_dgrad(dy, w, out_dtype=bf, epi=L.EPI_GELU_BWD, pre=pre, dbias=db)  # noqa: E731
+            else:
+                run = lambda: ops.linear_dgrad(dy, w, out_dtype=bf)  # noqa: E731
             nk, tiles = N // 64, ((M + 255) // 256) * (K // 256)
         for _ in range(30):  # warm clocks
             run()
@@ -99,6 +105,12 @@ def main():
         rec = {"class": kind, "shape": nm, "M": M, "nk": nk, "tiles": tiles, "wgs": int(st.shape[0]), "tpw": a.tpw,
                "dbg": a.dbg, "sched": a.sched}
         rec.update(analyse(st, nk, 64))
+        if kind == "gelu":  # epilogue phases (slots 50, 51): act' landed, products + column sums done
+            ok = st[:, 50] != 0
+            e0 = st[ok, 3 + nk]
+            rec["gelu_wait"] = int(np.mean(st[ok, 50] - e0))
+            rec["gelu_mul_csum"] = int(np.mean(st[ok, 51] - st[ok, 50]))
+            rec["gelu_sweep"] = int(np.mean(st[ok, 4 + nk] - st[ok, 51]))
         span = (st[:, 63].max() - st[:, 0].min()) / 100.0
         rec["span_us"] = round(float(span), 1)
         print(json.dumps(rec), flush=True)

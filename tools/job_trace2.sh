@@ -4,8 +4,6 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out
-timeout -k 10 300 python -u tools/bench_g4.py --wt --rounds 1 --shapes dgrad_qkv,dgrad_fc1,dgrad_proj > gpurun_out/bench_g4_wt.jsonl || exit 1
-cat gpurun_out/bench_g4_wt.jsonl
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_this -o run -- \
   python3 bench.py --steps 10 --warmup 3 --no-cpu --no-c3 > gpurun_out/bench_this_underprof.json 2> gpurun_out/prof_this.err || exit 1
 ( cd gpurun_ab/r05 && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_r05" -o run -- \

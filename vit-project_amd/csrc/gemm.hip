@@ -107,28 +107,6 @@ __device__ __forceinline__ f32x4 epi4(const Epi& e, int i, int j, f32x4 v, int z
 }
 
 
-// Column sums of a wave's epilogue outputs over one 64-row group (4 accumulator
-// rows of 16): cs[b] holds this lane's partial for columns j..j+3 of fragment b;
-// reduce over the 16 lanes of each row group and store one partial row.
-template <int AJ>
-__device__ __forceinline__ void csum_flush(const Epi& e, f32x4 (&cs)[AJ], int row0, int M, int N, int jbase, int lane) {
-#pragma unroll
-  for (int b = 0; b < AJ; ++b) {
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      float v = cs[b][t];
-      v += __shfl_xor(v, 1, 64);
-      v += __shfl_xor(v, 2, 64);
-      v += __shfl_xor(v, 4, 64);
-      v += __shfl_xor(v, 8, 64);
-      cs[b][t] = v;
-    }
-    const int j = jbase + b * 16 + 4 * (lane >> 4);
-    if ((lane & 15) == 0 && row0 < M && j < N)
-      *reinterpret_cast<f32x4*>(e.csum + (int64_t)(row0 >> 6) * N + j) = cs[b];
-    cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Row-contiguous epilogue (the bf16 fast kernels): V = 16 / sizeof(TO) consecutive
@@ -1363,10 +1341,11 @@ static int num_cus() {
   return n;
 }
 
-// g4 (gemm_g4.hip): the plain bf16 forward / input-gradient GEMMs.  g4_enabled(): VIT_GEMM_G4=0 sends these
-// classes back to the 8-wave V5 / V1 / V3 kernels (A/B); g4_launch returns -1 for shapes it does not take.
+// g4 (gemm_g4.hip): the plain bf16 forward / input-gradient GEMMs (ep 0) and the GELU' input gradient (ep
+// 1, VIT_G4_GELU).  g4_enabled(): VIT_GEMM_G4=0 sends these classes back to the 8-wave V5 / V1 / V3 kernels
+// (A/B); g4_launch returns -1 for shapes it does not take.
 bool g4_enabled();
-int g4_launch(int q_layout, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
+int g4_launch(int q_layout, int ep, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
               const Epi& e, hipStream_t s);
 // row-tile band of the tile walk per class (tile_coords); VIT_GEMM_GROUP_{FWD,DGRAD}=<row tiles> (A/B)
 // Bands of 8 row tiles help the wide-output GEMMs whose weight operand does not fit beside the
@@ -1396,7 +1375,15 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
     // the plain bf16 forward / input gradient: g4 by default (variant 20 forces it; any other forced
     // variant, a timing flag or VIT_GEMM_G4=0 keeps the 8-wave kernels)
     if (v == 20 || (g4_enabled() && g_variant < 0 && !e.dbg)) {
-      const int rc = g4_launch(QL, P, ldp, Q, ldq, M, N, R, split, e, s);
+      const int rc = g4_launch(QL, 0, P, ldp, Q, ldq, M, N, R, split, e, s);
+      if (rc != -1) return rc;
+    }
+  }
+  if constexpr (PL == LAY_RC && QL == LAY_CR && (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) &&
+                std::is_same<TO, bf16>::value && std::is_same<TA, bf16>::value) {
+    // the GELU' input gradient (C = dY W * act'): g4 when VIT_G4_GELU=1 (or variant 20)
+    if (v == 20 || (g4_enabled() && g_variant < 0 && !e.dbg)) {
+      const int rc = g4_launch(QL, 1, P, ldp, Q, ldq, M, N, R, split, e, s);
       if (rc != -1) return rc;
     }
   }

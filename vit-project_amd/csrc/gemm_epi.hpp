@@ -39,6 +39,29 @@ __device__ __forceinline__ void store_pair_bf16(void* base, int64_t ldc, int i, 
 }
 
 
+// Column sums of a wave's epilogue outputs over one 64-row group (4 accumulator
+// rows of 16): cs[b] holds this lane's partial for columns j..j+3 of fragment b;
+// reduce over the 16 lanes of each row group and store one partial row.
+template <int AJ>
+__device__ __forceinline__ void csum_flush(const Epi& e, f32x4 (&cs)[AJ], int row0, int M, int N, int jbase, int lane) {
+#pragma unroll
+  for (int b = 0; b < AJ; ++b) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float v = cs[b][t];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      cs[b][t] = v;
+    }
+    const int j = jbase + b * 16 + 4 * (lane >> 4);
+    if ((lane & 15) == 0 && row0 < M && j < N)
+      *reinterpret_cast<f32x4*>(e.csum + (int64_t)(row0 >> 6) * N + j) = cs[b];
+    cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
 namespace big {
 // Tile t of a tiles_i x tiles_j grid.  group_m == 0: row-major (consecutive t share a row tile,
 // so the P rows stay in the XCD's L2 while every Q column block streams past).  group_m > 0:

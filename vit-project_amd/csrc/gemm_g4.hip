@@ -104,7 +104,7 @@ __host__ __device__ __forceinline__ int tiles_of(const Walk& s, int w) {
 // fragment write's 16 rows hit distinct banks) and stores it row-contiguously
 constexpr int PITCH = 256 * 2 + 16, EPI_LDS = 256 * PITCH, RING_LDS = 5 * PIMG;  // P 3 deep + Q 2 deep at most
 constexpr int KERNEL_LDS = EPI_LDS > RING_LDS ? EPI_LDS : RING_LDS;
-static_assert(KERNEL_LDS <= 163840, "LDS");
+static_assert(KERNEL_LDS <= 163840 && EPI_LDS == 131072 + 4 * 1024, "LDS: the GELU' act' image = 2 stage slots + 4 pieces");
 constexpr int NST = 32;  // epilogue store instructions per thread (either form), issued unconditionally
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
@@ -124,7 +124,22 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // end, then s_memtime per event from slot 2 on: prologue done, every k-step's start, every epilogue's
 // start and end (up to slot 61).  SD >= 0 selects it, with timing switches SD & 7 (1 = no in-loop operand
 // loads, 2 = no in-loop barriers, 4 = no epilogue stores; results wrong, timing only) and schedule SD >> 4.
-template <int QL, int SD>
+// sum over a 16-lane row, every lane getting it: xor 1, xor 2 (quad_perm), then the quads and the halves
+// paired by row_half_mirror / row_mirror -- the pairs of a xor 4 / xor 8 butterfly, so the same sums bit for
+// bit as csum_flush's __shfl_xor form, without its ds_bpermute address registers
+// (inline asm: the builtin form's adds were paired into v_pk_add_f32, which takes no DPP operand, leaving a
+// v_mov_b32_dpp per step; the s_nop 1 covers the VALU-write -> DPP-read hazard the asm hides from the compiler)
+__device__ __forceinline__ float sum16_dpp(float v) {
+  asm volatile(
+      "s_nop 1\n v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n v_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+      "s_nop 1\n v_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1"
+      : "+v"(v));
+  return v;
+}
+
+template <int QL, int SD, int EP = 0>
 __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P, int64_t ldp,
                                                      const bf16* __restrict__ Q, int64_t ldq, int M, int N, int R,
                                                      Epi e, Walk s, unsigned long long* __restrict__ stamps) {
@@ -156,6 +171,7 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wi = wave >> 1, wj = wave & 1;
   const int nk = R / BK;
+  const int s_total = ntiles * nk;  // stages of this workgroup's stream
 
   // ---- loaders: P and Q each keep the tile and k-step of the next stage they issue (P runs DP - 2 stages
   // ahead of Q) and that tile's per-lane source offsets.  LDS: DP = 2: two [P | Q] stage slots (the P
@@ -198,8 +214,33 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
   set_p(true);
   set_q(true);
   const int64_t qstep = QL == LAY_RC ? (int64_t)BK * 2 : (int64_t)BK * ldq * 2;  // bytes per k-step
-  auto pbase = [&]() { return reinterpret_cast<const char*>(P) + (int64_t)kP * BK * 2; };
-  auto qbase = [&]() { return reinterpret_cast<const char*>(Q) + (int64_t)kQ * qstep; };
+  // EP 1 (GELU' input gradient, one tile per workgroup): the two stages past the stream's end carry the
+  // tile's act' image instead of re-reads, in the epilogue's [256][PITCH] bf16 layout: the stage slots hold
+  // image bytes [0, 128 KiB) (the slot aux stage a fills, (s_total + a) % 2, bytes [64 KiB * slot, + 64
+  // KiB); P pieces the first half of a slot, Q pieces the second), one more piece per wave (after the
+  // first aux k-step's second barrier) the last 4 KiB.  The DMA source picks the 16 B of LDS chunk p:
+  // image row p / 33, chunk p % 33 (32 = the row pad: any valid address).
+  auto aux_off = [&](int p) {
+    const int row = p / 33, c = min(p - row * 33, 31);
+    return (uint32_t)((int64_t)min(i0P + row, M - 1) * e.ld_aux * 2 + (int64_t)min(jP + c * 8, N - 8) * 2);
+  };
+  auto set_aux = [&](uint32_t (&off)[8], int half, int a) {
+    const int slot = (s_total + a) & 1;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) off[u] = aux_off(slot * 4096 + (half * 32 + wave * 8 + u) * 64 + lane);
+  };
+  auto pbase = [&]() {
+    if constexpr (EP == 1) {
+      if (qP >= ntiles) return reinterpret_cast<const char*>(e.aux);
+    }
+    return reinterpret_cast<const char*>(P) + (int64_t)kP * BK * 2;
+  };
+  auto qbase = [&]() {
+    if constexpr (EP == 1) {
+      if (qQ >= ntiles) return reinterpret_cast<const char*>(e.aux);
+    }
+    return reinterpret_cast<const char*>(Q) + (int64_t)kQ * qstep;
+  };
   auto piece_p = [&](int u, const char* pb, char* buf) {
     __builtin_amdgcn_global_load_lds((const void*)(pb + offP[u]), LDS_PTR(buf + (wave * 8 + u) * 1024), 16, 0, 0);
   };
@@ -212,12 +253,18 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
       ++qP;
       set_p(tile_at(s, w, qP, i0P, jP));
     }
+    if constexpr (EP == 1) {
+      if (qP == ntiles && kP < 2) set_aux(offP, 0, kP);  // i0P / jP stay the last tile's
+    }
   };
   auto advance_q = [&]() {
     if (++kQ == nk) {
       kQ = 0;
       ++qQ;
       set_q(tile_at(s, w, qQ, iQ, j0Q));
+    }
+    if constexpr (EP == 1) {
+      if (qQ == ntiles && kQ < 2) set_aux(offQ, 1, kQ);
     }
   };
 
@@ -335,6 +382,11 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
             read_frag(std::integral_constant<int, 1>{}, std::integral_constant<int, (m - SC::Y0) / SC::YS>{}, cp, cq, pY, qY);
           if constexpr (m >= SC::X0 && (m - SC::X0) % SC::XS == 0 && (m - SC::X0) / SC::XS < 16)
             read_frag(std::integral_constant<int, 0>{}, std::integral_constant<int, (m - SC::X0) / SC::XS>{}, np, nq, pX, qX);
+          if constexpr (EP == 1 && m == SC::B2 + 1) {
+            if (g + 2 == s_total)  // aux stage 0's k-step, after its second barrier: the next k-step's wait counts it
+              __builtin_amdgcn_global_load_lds((const void*)(pb + aux_off(8192 + wave * 64 + lane)),
+                                               LDS_PTR(smem + 131072 + wave * 1024), 16, 0, 0);
+          }
           if constexpr (m >= SC::P0 && (m - SC::P0) % SC::PS == 0 && (m - SC::P0) / SC::PS < 16) {
             constexpr int u = (m - SC::P0) / SC::PS;
             constexpr int v = SC::PF ? u : (u & 1) * 8 + (u >> 1);  // 0..7 P pieces, 8..15 Q pieces
@@ -361,6 +413,67 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
     __builtin_amdgcn_sched_barrier(0);
     stamp();
     const int gq = lane >> 4;
+    if constexpr (EP == 1) {
+      // the tile origin re-defined here: nothing derived from it is hoisted above the k-step loop (the
+      // column-partial addresses would be, and spill)
+      int ti0 = i0, tj0 = j0;
+      asm volatile("" : "+s"(ti0), "+s"(tj0));
+      // C = bf16(acc * act'), the product written over its act' in the LDS image, then 512-B row segments
+      // out; e.csum: per 64-row group column partials of the f32 products (the 8-wave kernels' fragment
+      // epilogue order: a lane's 4 rows in order, then the 16-lane butterfly)
+      auto mark = [&](int k) {  // stamped instance: phases of this epilogue in slots 50..52
+        if constexpr (STAMP) {
+          if (tid == 0) stamps[(int64_t)blockIdx.x * 64 + 50 + k] = __builtin_amdgcn_s_memtime();
+        }
+      };
+      big::wait_vm<0>();
+      big::lds_barrier();
+      mark(0);
+      f32x4 cs[8];
+#pragma unroll
+      for (int b = 0; b < 8; ++b) cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int a = 0; a < 8; ++a) {
+        asm volatile("" : "+a"(acc[a][0]), "+a"(acc[a][1]), "+a"(acc[a][2]), "+a"(acc[a][3]), "+a"(acc[a][4]),
+                          "+a"(acc[a][5]), "+a"(acc[a][6]), "+a"(acc[a][7]));
+        const int r = wi * 128 + a * 16 + (lane & 15);
+        const float rowin = ti0 + r < M ? 1.f : 0.f;  // rows past M (clamped copies of row M - 1) add nothing
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+          char* const p = smem + r * PITCH + (wj * 128 + b * 16 + 4 * gq) * 2;
+          const bf16x4 d = *reinterpret_cast<const bf16x4*>(p);
+          const f32x4 v = acc[a][b] * f32x4{(float)d[0], (float)d[1], (float)d[2], (float)d[3]};
+          *reinterpret_cast<bf16x4*>(p) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
+#pragma unroll
+          for (int t = 0; t < 4; ++t) cs[b][t] = __builtin_fmaf(v[t], rowin, cs[b][t]);  // = cs + v, or cs
+        }
+        if ((a & 3) == 3) {  // csum_flush's 16-lane butterfly as DPP adds (same pairs: same sums)
+          const int row0 = ti0 + wi * 128 + (a - 3) * 16;
+#pragma unroll
+          for (int b = 0; b < 8; ++b) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) cs[b][t] = sum16_dpp(cs[b][t]);
+            const int j = tj0 + wj * 128 + b * 16 + 4 * gq;
+            if (e.csum && (lane & 15) == 0 && row0 < M && j < N)
+              *reinterpret_cast<f32x4*>(e.csum + (int64_t)(row0 >> 6) * N + j) = cs[b];
+            cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      big::lds_barrier();
+      mark(1);
+      const int c = tid & 31, r0 = tid >> 5;
+      const int col = tj0 + c * 8;
+#pragma unroll 8
+      for (int p = 0; p < NST; ++p) {
+        const int r = r0 + 8 * p;
+        const i32x4 v = *reinterpret_cast<const i32x4*>(smem + r * PITCH + c * 16);
+        store16(v, i0 + r, col, ti0 + r < M && col < N);
+      }
+      stamp();
+      continue;
+    }
     f32x4 bias4[8];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -430,7 +543,7 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
 namespace {
 // VIT_GEMM_G4 (0 = off), VIT_G4_MODE_{FWD,DGRAD} (0 stride, 1 band), VIT_G4_WGS (stride-walk grid cap),
 // VIT_G4_TPW (stride walk: at most this many tiles per workgroup, 0 = no limit)
-int g_g4[6] = {-2, -2, -2, -2, -2, -2};
+int g_g4[7] = {-2, -2, -2, -2, -2, -2, -2};
 int g_g4_dbg = 0;  // timing switches of the stamped instance (vit_debug_g4_stamps)
 unsigned g_g4_launches = 0;  // host-side count of g4 launches (tests: the plain GEMMs took this kernel)
 unsigned long long* g_g4_stamps = nullptr;  // vit_debug_g4_stamps: launch the stamped instance
@@ -447,6 +560,7 @@ void g4_env() {
   g_g4[4] = g4_env_int("VIT_G4_TPW", 1);  // in the step one tile per workgroup measured best for the
                                           // forward (7267 vs 7061-7091 img/s for 2, 3, 3.8 tiles / CU)
   g_g4[5] = g4_env_int("VIT_G4_EPI", 0);
+  g_g4[6] = g4_env_int("VIT_G4_GELU", 1);  // the GELU' input gradient on g4 (EP 1): +0.5 % in the step
 }
 int g4_cus() {
   static int n = 0;
@@ -458,9 +572,13 @@ int g4_cus() {
   return n;
 }
 template <int QL>
-int launch(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, const Epi& e, hipStream_t s) {
+int launch(int ep, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, const Epi& e, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
+    if constexpr (QL == LAY_CR) {
+      (void)hipFuncSetAttribute((const void*)g4::kernel<QL, -1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::KERNEL_LDS);
+      (void)hipFuncSetAttribute((const void*)g4::kernel<QL, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::KERNEL_LDS);
+    }
     for (const void* k : {(const void*)g4::kernel<QL, -1>, (const void*)g4::kernel<QL, 0>, (const void*)g4::kernel<QL, 1>,
                           (const void*)g4::kernel<QL, 2>, (const void*)g4::kernel<QL, 4>, (const void*)g4::kernel<QL, 16>,
                           (const void*)g4::kernel<QL, 32>, (const void*)g4::kernel<QL, 48>, (const void*)g4::kernel<QL, 64>})
@@ -484,6 +602,17 @@ int launch(const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N,
     hipLaunchKernelGGL(kern, dim3(w.G), dim3(g4::THREADS), g4::KERNEL_LDS, s, (const bf16*)P, ldp, (const bf16*)Q, ldq,
                        M, N, R, e, w, g_g4_stamps);
   };
+  if constexpr (QL == LAY_CR) {
+    if (ep == 1) {  // the GELU' input gradient (g4_launch checked it): one tile per workgroup, bands of group_m
+      w.mode = 0;
+      w.group_m = e.group_m;
+      w.G = w.tiles_i * w.tiles_j;
+      if (g_g4_stamps) go(g4::kernel<QL, 0, 1>);
+      else go(g4::kernel<QL, -1, 1>);
+      ++g_g4_launches;
+      return (int)hipGetLastError();
+    }
+  }
   if (!g_g4_stamps) {
     go(g4::kernel<QL, -1>);
   } else {
@@ -510,13 +639,20 @@ bool g4_enabled() {
 
 // the plain bf16 GEMM C = P Q^T (+ bias) on g4, or -1 when the shape is not one it takes: a split
 // reduction, column sums, slab output, R % 64, N % 8 (the dispatcher then runs the 8-wave kernels)
-int g4_launch(int q_layout, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
+int g4_launch(int q_layout, int ep, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M, int N, int R, int split,
               const Epi& e, hipStream_t s) {
   g4_env();
-  if (split > 1 || R <= 0 || R % g4::BK || N < 8 || N % 8 || e.csum || e.slab || M <= 0) return -1;
+  if (split > 1 || R <= 0 || R % g4::BK || N < 8 || N % 8 || e.slab || M <= 0) return -1;
   if ((int64_t)M * e.ldc * 2 >= ((int64_t)1 << 31) || e.ldc % 8) return -1;  // buffer-store offsets are int32
-  return q_layout == LAY_RC ? launch<LAY_RC>(P, ldp, Q, ldq, M, N, R, e, s)
-                            : launch<LAY_CR>(P, ldp, Q, ldq, M, N, R, e, s);
+  if (ep == 1) {  // GELU' input gradient: C = (P Q^T) * aux, column partials allowed; no bias
+    if (!g_g4[6] || q_layout != LAY_CR || !e.aux || e.bias || R < 2 * g4::BK || e.ld_aux % 8 || ((uintptr_t)e.aux & 15) ||
+        (int64_t)M * e.ld_aux * 2 >= ((int64_t)1 << 31))
+      return -1;
+    return launch<LAY_CR>(1, P, ldp, Q, ldq, M, N, R, e, s);
+  }
+  if (e.csum) return -1;
+  return q_layout == LAY_RC ? launch<LAY_RC>(0, P, ldp, Q, ldq, M, N, R, e, s)
+                            : launch<LAY_CR>(0, P, ldp, Q, ldq, M, N, R, e, s);
 }
 
 extern "C" {
@@ -540,6 +676,15 @@ int vit_debug_g4_stamps(void* buf, int dbg) {
   g_g4_stamps = (unsigned long long*)buf;
   g_g4_dbg = dbg;
   return 0;
+}
+
+// Tuning / test hook: the GELU' input gradient on g4 (1) or on the 8-wave kernels (0); -1 keeps.  Returns the
+// previous setting.
+int vit_gemm_g4_gelu(int on) {
+  g4_env();
+  const int prev = g_g4[6];
+  if (on >= 0) g_g4[6] = on;
+  return prev;
 }
 
 // Host-side count of g4 launches since the last reset (reset != 0 zeroes it after reading).

@@ -29,6 +29,7 @@ SIGNATURES = {
     "vit_gemm_group": [i32, i32],
     "vit_gemm_g4_config": [i32, i32, i32, i32],
     "vit_gemm_g4_count": [i32],
+    "vit_gemm_g4_gelu": [i32],
     "vit_gemm_streamk_workspace": [vp, vp, i64, vp, i32],
     "vit_gemm_rc_chunk_rows": [i32, i64],
     "vit_gemm": [i32, i32, i32, i32, i32, i32, i32, i32, vp, i64, vp, i64, vp, i64, vp, vp, i64, vp, i32, vp],
