@@ -663,6 +663,38 @@ def test_g4_gelu_dgrad_matches_v1(M, K, N):
     _close(db4, ref.sum(0).float(), 1e-4, "fused column sums vs fp64")
 
 
+@pytest.mark.parametrize("M,N,K", [(27580, 3072, 768), (22852, 3072, 768), (1000, 3072, 768), (257, 136, 192),
+                                   (1, 64, 64), (300, 1088, 128)])
+def test_g4_gelu_pair_forward_matches_v5(M, N, K):
+    """The fc1 forward with its GELU pair epilogue (C = GELU'(pre), act = GELU(pre), pre = bf16(x W^T + b)) on
+    g4 (vit_gemm_g4_gelu bit 1: pre through the LDS image, the pair computed in the row sweep) against the
+    8-wave V5 kernel forced, at the two forward chains' row counts and ragged shapes: both outputs BIT FOR BIT
+    (same k order, same pre rounding, the same gelu_fast_both), and within bf16 rounding of the exact-erf
+    GELU / GELU' of an fp64 pre."""
+    lib = L.lib()
+    bf = torch.bfloat16
+    x = _rnd(M, K, seed=M + K + 21).to(bf).to(DEV)
+    w = (_rnd(N, K, seed=N * K + 4) * 0.05).to(bf).to(DEV)
+    b = _rnd(N, seed=9).to(DEV)
+    prev = lib.vit_gemm_g4_gelu(3)
+    try:
+        lib.vit_gemm_g4_count(1)
+        d4, a4 = ops.linear_fwd(x, w, b, epi=L.EPI_BIAS_GELU)
+        torch.cuda.synchronize()
+        assert lib.vit_gemm_g4_count(1) == 1, "the GELU pair did not run on g4"
+        lib.vit_gemm_variant(5)
+        d5, a5 = ops.linear_fwd(x, w, b, epi=L.EPI_BIAS_GELU)
+        torch.cuda.synchronize()
+    finally:
+        lib.vit_gemm_variant(-1)
+        lib.vit_gemm_g4_gelu(prev)
+    assert torch.equal(d4, d5), "g4 GELU' (C) differs from V5"
+    assert torch.equal(a4, a5), "g4 GELU (act) differs from V5"
+    pre = (x.double() @ w.double().t() + b.double()).to(bf).double()
+    _close(a4, torch.nn.functional.gelu(pre).float(), 8e-3, "act vs fp64 erf GELU")
+    _close(d4, _gelu_grad(pre).float(), 8e-3, "GELU' vs fp64")
+
+
 # ---------------------------------------------------------------------------- LayerNorm
 
 @pytest.mark.parametrize("D", [768, 1024, 64, 200])

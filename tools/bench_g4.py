@@ -119,6 +119,20 @@ def gelu(a):
             rec.setdefault(tag, []).append(round(flop / timeit(fn, a.reps) / 1e12, 1))
             lib.vit_gemm_g4_gelu(prev)
     print(json.dumps(rec), flush=True)
+    for Mf in (27580, 22852):  # the fc1 GELU pair forward at the two chains' rows: g4 (mask 3) vs V5 (mask 1)
+        x = torch.randn(Mf, N, device=dev, generator=g).to(bf)
+        w1 = (torch.randn(K, N, device=dev, generator=g) * 0.05).to(bf)
+        b1 = torch.randn(K, device=dev, generator=g)
+        d, act = torch.empty(Mf, K, device=dev, dtype=bf), torch.empty(Mf, K, device=dev, dtype=bf)
+        fn = lambda: ops.linear_fwd(x, w1, b1, epi=L.EPI_BIAS_GELU, out=d, act_out=act)  # noqa: E731
+        flop = 2.0 * Mf * N * K
+        rec = {"class": "gelu_pair_fwd", "M": Mf, "N": K, "K": N}
+        for _ in range(a.rounds):
+            for tag, on in (("g4", 3), ("V5", 1)):
+                prev = lib.vit_gemm_g4_gelu(on)
+                rec.setdefault(tag, []).append(round(flop / timeit(fn, a.reps) / 1e12, 1))
+                lib.vit_gemm_g4_gelu(prev)
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":

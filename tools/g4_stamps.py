@@ -111,6 +111,8 @@ def main():
             rec["gelu_wait"] = int(np.mean(st[ok, 50] - e0))
             rec["gelu_mul_csum"] = int(np.mean(st[ok, 51] - st[ok, 50]))
             rec["gelu_sweep"] = int(np.mean(st[ok, 4 + nk] - st[ok, 51]))
+            ks = np.diff(st[ok, 3:4 + nk].astype(np.int64), axis=1)  # k-step k's cycles (k = 0 .. nk-1)
+            rec["kstep_by_k"] = [int(x) for x in ks.mean(axis=0)]
         span = (st[:, 63].max() - st[:, 0].min()) / 100.0
         rec["span_us"] = round(float(span), 1)
         print(json.dumps(rec), flush=True)

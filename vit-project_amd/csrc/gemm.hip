@@ -1379,6 +1379,13 @@ static int launch_fast(const void* P, int64_t ldp, const void* Q, int64_t ldq, i
       if (rc != -1) return rc;
     }
   }
+  if constexpr (PL == LAY_RC && QL == LAY_RC && EPI == EPI_BIAS_GELU && std::is_same<TO, bf16>::value) {
+    // the fc1 GELU pair forward: g4 when bit 1 of VIT_G4_GELU / vit_gemm_g4_gelu is set
+    if (v == 20 || (g4_enabled() && g_variant < 0 && !e.dbg)) {
+      const int rc = g4_launch(QL, 2, P, ldp, Q, ldq, M, N, R, split, e, s);
+      if (rc != -1) return rc;
+    }
+  }
   if constexpr (PL == LAY_RC && QL == LAY_CR && (EPI == EPI_GELU_BWD || EPI == EPI_QGELU_BWD) &&
                 std::is_same<TO, bf16>::value && std::is_same<TA, bf16>::value) {
     // the GELU' input gradient (C = dY W * act'): g4 when VIT_G4_GELU=1 (or variant 20)

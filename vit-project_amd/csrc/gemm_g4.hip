@@ -124,19 +124,24 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // end, then s_memtime per event from slot 2 on: prologue done, every k-step's start, every epilogue's
 // start and end (up to slot 61).  SD >= 0 selects it, with timing switches SD & 7 (1 = no in-loop operand
 // loads, 2 = no in-loop barriers, 4 = no epilogue stores; results wrong, timing only) and schedule SD >> 4.
-// sum over a 16-lane row, every lane getting it: xor 1, xor 2 (quad_perm), then the quads and the halves
-// paired by row_half_mirror / row_mirror -- the pairs of a xor 4 / xor 8 butterfly, so the same sums bit for
-// bit as csum_flush's __shfl_xor form, without its ds_bpermute address registers
-// (inline asm: the builtin form's adds were paired into v_pk_add_f32, which takes no DPP operand, leaving a
-// v_mov_b32_dpp per step; the s_nop 1 covers the VALU-write -> DPP-read hazard the asm hides from the compiler)
-__device__ __forceinline__ float sum16_dpp(float v) {
-  asm volatile(
-      "s_nop 1\n v_add_f32_dpp %0, %0, %0 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-      "s_nop 1\n v_add_f32_dpp %0, %0, %0 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-      "s_nop 1\n v_add_f32_dpp %0, %0, %0 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-      "s_nop 1\n v_add_f32_dpp %0, %0, %0 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1"
-      : "+v"(v));
-  return v;
+// sums over a 16-lane row of four values, every lane getting them: xor 1, xor 2 (quad_perm), then the quads
+// and the halves paired by row_half_mirror / row_mirror -- the pairs of a xor 4 / xor 8 butterfly, so the
+// same sums bit for bit as csum_flush's __shfl_xor form.  Inline asm (the builtin form's adds were paired
+// into v_pk_add_f32, which takes no DPP operand): four independent chains interleaved put 4 instructions
+// between a DPP add and the next read of its result; the leading s_nop 1 covers the VALU write -> DPP read
+// hazard for the inputs, which the asm hides from the compiler.
+__device__ __forceinline__ void sum16_dpp4(f32x4& v) {
+  float a = v[0], b = v[1], c = v[2], d = v[3];
+#define G4_DPP4(CTRL)                                                                \
+  "v_add_f32_dpp %0, %0, %0 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n"     \
+  "v_add_f32_dpp %1, %1, %1 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n"     \
+  "v_add_f32_dpp %2, %2, %2 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n"     \
+  "v_add_f32_dpp %3, %3, %3 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+  asm volatile("s_nop 1\n" G4_DPP4("quad_perm:[1,0,3,2]") G4_DPP4("quad_perm:[2,3,0,1]") G4_DPP4("row_half_mirror")
+                   G4_DPP4("row_mirror")
+               : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+#undef G4_DPP4
+  v = f32x4{a, b, c, d};
 }
 
 template <int QL, int SD, int EP = 0>
@@ -149,7 +154,7 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
   if (ntiles <= 0) return;
   const int tid = threadIdx.x, lane = tid & 63;
   constexpr bool STAMP = SD >= 0;
-  constexpr int dbg = SD < 0 ? 0 : (SD & 7);  // compile-time: the switches cost the timed instance nothing
+  constexpr int dbg = SD < 0 ? 0 : (SD & 15);  // 8 (EP 1): no act' offsets (garbage image; timing only)  // compile-time: the switches cost the timed instance nothing
   using SC = Sched<SD < 0 ? 0 : (SD >> 4)>;
   constexpr int NB2 = pieces_before_b2<SC>();
   int ev = 2;
@@ -220,9 +225,11 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
   // KiB); P pieces the first half of a slot, Q pieces the second), one more piece per wave (after the
   // first aux k-step's second barrier) the last 4 KiB.  The DMA source picks the 16 B of LDS chunk p:
   // image row p / 33, chunk p % 33 (32 = the row pad: any valid address).
+  const int ldaux2 = (int)e.ld_aux * 2;  // < 2^24 (g4_launch): 24-bit multiplies below
   auto aux_off = [&](int p) {
-    const int row = p / 33, c = min(p - row * 33, 31);
-    return (uint32_t)((int64_t)min(i0P + row, M - 1) * e.ld_aux * 2 + (int64_t)min(jP + c * 8, N - 8) * 2);
+    const int row = (p * 1986) >> 16;  // p / 33 for p < 8448 (the image's chunks)
+    const int c = min(p - row * 33, 31);
+    return __umul24((unsigned)min(i0P + row, M - 1), (unsigned)ldaux2) + (unsigned)min(jP + c * 8, N - 8) * 2u;
   };
   auto set_aux = [&](uint32_t (&off)[8], int half, int a) {
     const int slot = (s_total + a) & 1;
@@ -254,7 +261,7 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
       set_p(tile_at(s, w, qP, i0P, jP));
     }
     if constexpr (EP == 1) {
-      if (qP == ntiles && kP < 2) set_aux(offP, 0, kP);  // i0P / jP stay the last tile's
+      if (!(dbg & 8) && qP == ntiles && kP < 2) set_aux(offP, 0, kP);  // i0P / jP stay the last tile's
     }
   };
   auto advance_q = [&]() {
@@ -264,7 +271,7 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
       set_q(tile_at(s, w, qQ, iQ, j0Q));
     }
     if constexpr (EP == 1) {
-      if (qQ == ntiles && kQ < 2) set_aux(offQ, 1, kQ);
+      if (!(dbg & 8) && qQ == ntiles && kQ < 2) set_aux(offQ, 1, kQ);
     }
   };
 
@@ -416,8 +423,9 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
     if constexpr (EP == 1) {
       // the tile origin re-defined here: nothing derived from it is hoisted above the k-step loop (the
       // column-partial addresses would be, and spill)
-      int ti0 = i0, tj0 = j0;
-      asm volatile("" : "+s"(ti0), "+s"(tj0));
+      int ti0 = i0, tj0 = j0, el = lane;
+      asm volatile("" : "+s"(ti0), "+s"(tj0), "+v"(el));
+      const int eg = el >> 4, e15 = el & 15;
       // C = bf16(acc * act'), the product written over its act' in the LDS image, then 512-B row segments
       // out; e.csum: per 64-row group column partials of the f32 products (the 8-wave kernels' fragment
       // epilogue order: a lane's 4 rows in order, then the 16-lane butterfly)
@@ -436,25 +444,24 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
       for (int a = 0; a < 8; ++a) {
         asm volatile("" : "+a"(acc[a][0]), "+a"(acc[a][1]), "+a"(acc[a][2]), "+a"(acc[a][3]), "+a"(acc[a][4]),
                           "+a"(acc[a][5]), "+a"(acc[a][6]), "+a"(acc[a][7]));
-        const int r = wi * 128 + a * 16 + (lane & 15);
+        const int r = wi * 128 + a * 16 + e15;
         const float rowin = ti0 + r < M ? 1.f : 0.f;  // rows past M (clamped copies of row M - 1) add nothing
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
-          char* const p = smem + r * PITCH + (wj * 128 + b * 16 + 4 * gq) * 2;
+          char* const p = smem + r * PITCH + (wj * 128 + b * 16 + 4 * eg) * 2;
           const bf16x4 d = *reinterpret_cast<const bf16x4*>(p);
           const f32x4 v = acc[a][b] * f32x4{(float)d[0], (float)d[1], (float)d[2], (float)d[3]};
           *reinterpret_cast<bf16x4*>(p) = bf16x4{(bf16)v[0], (bf16)v[1], (bf16)v[2], (bf16)v[3]};
 #pragma unroll
           for (int t = 0; t < 4; ++t) cs[b][t] = __builtin_fmaf(v[t], rowin, cs[b][t]);  // = cs + v, or cs
         }
-        if ((a & 3) == 3) {  // csum_flush's 16-lane butterfly as DPP adds (same pairs: same sums)
+        if ((a & 3) == 3) {  // one partial row per 64-row group
           const int row0 = ti0 + wi * 128 + (a - 3) * 16;
 #pragma unroll
           for (int b = 0; b < 8; ++b) {
-#pragma unroll
-            for (int t = 0; t < 4; ++t) cs[b][t] = sum16_dpp(cs[b][t]);
-            const int j = tj0 + wj * 128 + b * 16 + 4 * gq;
-            if (e.csum && (lane & 15) == 0 && row0 < M && j < N)
+            sum16_dpp4(cs[b]);
+            const int j = tj0 + wj * 128 + b * 16 + 4 * eg;
+            if (e.csum && e15 == 0 && row0 < M && j < N)
               *reinterpret_cast<f32x4*>(e.csum + (int64_t)(row0 >> 6) * N + j) = cs[b];
             cs[b] = f32x4{0.f, 0.f, 0.f, 0.f};
           }
@@ -463,7 +470,7 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
       }
       big::lds_barrier();
       mark(1);
-      const int c = tid & 31, r0 = tid >> 5;
+      const int c = el & 31, r0 = wave * 2 + (el >> 5);
       const int col = tj0 + c * 8;
 #pragma unroll 8
       for (int p = 0; p < NST; ++p) {
@@ -484,7 +491,7 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
     // group gq then holds 8 columns of the pair).  The last tile (staged): once the stream-end pieces have
     // landed and every wave's reads retired (wait + barrier) the stage slots are free, so the tile goes
     // through a bf16 LDS image and out in 512-B row segments.
-    const bool staged = !(q + 1 < ntiles || s.epi == 1);
+    const bool staged = EP == 2 || !(q + 1 < ntiles || s.epi == 1);  // EP 2: one tile per workgroup
     if (staged) {
       big::wait_vm<0>();
       big::lds_barrier();
@@ -519,11 +526,35 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
       big::lds_barrier();
       const int c = tid & 31, r0 = tid >> 5;
       const int col = j0 + c * 8;
+      if constexpr (EP == 2) {
+        // fc1's GELU pair: from the bf16 pre image (pre = bf16(acc + bias), as the 8-wave kernels' staged
+        // pair epilogue), C = GELU'(pre) and aux_out = GELU(pre) (gelu_fast_both), both 512-B row segments
+        const __amdgpu_buffer_rsrc_t ars =
+            __builtin_amdgcn_make_buffer_rsrc(e.aux_out, (short)0, (int)((int64_t)M * e.ldc * 2), 0x00020000);
+#pragma unroll 4
+        for (int p = 0; p < NST; ++p) {
+          const int r = r0 + 8 * p;
+          const bf16x8 x = *reinterpret_cast<const bf16x8*>(smem + r * PITCH + c * 16);
+          bf16x8 av, dv;
+#pragma unroll
+          for (int t = 0; t < 8; ++t) {
+            float ga, gd;
+            gelu_fast_both((float)x[t], ga, gd);
+            av[t] = (bf16)ga;
+            dv[t] = (bf16)gd;
+          }
+          const bool ok = i0 + r < M && col < N;
+          store16(__builtin_bit_cast(i32x4, dv), i0 + r, col, ok);
+          const int off = ok ? (int)(((int64_t)(i0 + r) * e.ldc + col) * 2) : (int)0x80000000;
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i32x4, av), ars, off, 0, 0);
+        }
+      } else {
 #pragma unroll 8
-      for (int p = 0; p < NST; ++p) {
-        const int r = r0 + 8 * p;
-        const i32x4 v = *reinterpret_cast<const i32x4*>(smem + r * PITCH + c * 16);
-        store16(v, i0 + r, col, i0 + r < M && col < N);
+        for (int p = 0; p < NST; ++p) {
+          const int r = r0 + 8 * p;
+          const i32x4 v = *reinterpret_cast<const i32x4*>(smem + r * PITCH + c * 16);
+          store16(v, i0 + r, col, i0 + r < M && col < N);
+        }
       }
     }
     stamp();
@@ -578,6 +609,10 @@ int launch(int ep, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M
     if constexpr (QL == LAY_CR) {
       (void)hipFuncSetAttribute((const void*)g4::kernel<QL, -1, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::KERNEL_LDS);
       (void)hipFuncSetAttribute((const void*)g4::kernel<QL, 0, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::KERNEL_LDS);
+      (void)hipFuncSetAttribute((const void*)g4::kernel<QL, 8, 1>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::KERNEL_LDS);
+    } else {
+      (void)hipFuncSetAttribute((const void*)g4::kernel<QL, -1, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::KERNEL_LDS);
+      (void)hipFuncSetAttribute((const void*)g4::kernel<QL, 0, 2>, hipFuncAttributeMaxDynamicSharedMemorySize, g4::KERNEL_LDS);
     }
     for (const void* k : {(const void*)g4::kernel<QL, -1>, (const void*)g4::kernel<QL, 0>, (const void*)g4::kernel<QL, 1>,
                           (const void*)g4::kernel<QL, 2>, (const void*)g4::kernel<QL, 4>, (const void*)g4::kernel<QL, 16>,
@@ -607,8 +642,19 @@ int launch(int ep, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M
       w.mode = 0;
       w.group_m = e.group_m;
       w.G = w.tiles_i * w.tiles_j;
-      if (g_g4_stamps) go(g4::kernel<QL, 0, 1>);
+      if (g_g4_stamps && g_g4_dbg == 8) go(g4::kernel<QL, 8, 1>);
+      else if (g_g4_stamps) go(g4::kernel<QL, 0, 1>);
       else go(g4::kernel<QL, -1, 1>);
+      ++g_g4_launches;
+      return (int)hipGetLastError();
+    }
+  } else {
+    if (ep == 2) {  // the fc1 GELU pair forward: one tile per workgroup, the forward's tile order
+      w.mode = 0;
+      w.group_m = e.group_m;
+      w.G = w.tiles_i * w.tiles_j;
+      if (g_g4_stamps) go(g4::kernel<QL, 0, 2>);
+      else go(g4::kernel<QL, -1, 2>);
       ++g_g4_launches;
       return (int)hipGetLastError();
     }
@@ -644,8 +690,13 @@ int g4_launch(int q_layout, int ep, const void* P, int64_t ldp, const void* Q, i
   g4_env();
   if (split > 1 || R <= 0 || R % g4::BK || N < 8 || N % 8 || e.slab || M <= 0) return -1;
   if ((int64_t)M * e.ldc * 2 >= ((int64_t)1 << 31) || e.ldc % 8) return -1;  // buffer-store offsets are int32
+  if (ep == 2) {  // fc1 GELU pair forward: C = GELU'(pre), aux_out = GELU(pre), pre = bf16(P Q^T + bias)
+    if (!(g_g4[6] & 2) || q_layout != LAY_RC || !e.aux_out || e.csum) return -1;
+    return launch<LAY_RC>(2, P, ldp, Q, ldq, M, N, R, e, s);
+  }
   if (ep == 1) {  // GELU' input gradient: C = (P Q^T) * aux, column partials allowed; no bias
-    if (!g_g4[6] || q_layout != LAY_CR || !e.aux || e.bias || R < 2 * g4::BK || e.ld_aux % 8 || ((uintptr_t)e.aux & 15) ||
+    if (!(g_g4[6] & 1) || q_layout != LAY_CR || !e.aux || e.bias || R < 2 * g4::BK || e.ld_aux % 8 || ((uintptr_t)e.aux & 15) ||
+        e.ld_aux >= (1 << 23) ||
         (int64_t)M * e.ld_aux * 2 >= ((int64_t)1 << 31))
       return -1;
     return launch<LAY_CR>(1, P, ldp, Q, ldq, M, N, R, e, s);
@@ -678,8 +729,8 @@ int vit_debug_g4_stamps(void* buf, int dbg) {
   return 0;
 }
 
-// Tuning / test hook: the GELU' input gradient on g4 (1) or on the 8-wave kernels (0); -1 keeps.  Returns the
-// previous setting.
+// Tuning / test hook: which GELU GEMMs run on g4 (bit 0: the GELU' input gradient, bit 1: the fc1 GELU pair
+// forward; the rest stay on the 8-wave kernels); -1 keeps.  Returns the previous mask.
 int vit_gemm_g4_gelu(int on) {
   g4_env();
   const int prev = g_g4[6];
