@@ -140,7 +140,8 @@ def cpu_baseline(seconds: float):
 # the sources the weight-gradient kernel is built from: a committed counter file records their hash
 # (tools/pmc_traffic.py / tools/pmc_step_classes.py --src-sha), so the bench line can say whether the
 # counters it quotes were taken on the kernel that ran
-WGRAD_SOURCES = ("vit-project_amd/csrc/gemm.hip", "vit-project_amd/csrc/gemm_lds.hpp", "vit-project_amd/csrc/gemm_w4.inc")
+WGRAD_SOURCES = ("vit-project_amd/csrc/gemm.hip", "vit-project_amd/csrc/gemm_lds.hpp", "vit-project_amd/csrc/gemm_w4.inc",
+                 "vit-project_amd/csrc/gemm_epi.hpp")
 
 
 def wgrad_src_sha():
