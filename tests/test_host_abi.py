@@ -54,6 +54,17 @@ def test_gemm_32bit_offset_plan():
     assert rows(1000, 1 << 25) == 0  # 64 MiB rows: no 256-row chunk fits, the fast path is refused
 
 
+def test_library_links_no_vendor_blas():
+    """Every GEMM of the path is hand-written since ABI 10 (round 6): the library's dynamic section names no
+    hipBLASLt / rocBLAS / hipBLAS, and no exported symbol mentions them."""
+    import subprocess
+    so = os.path.join(ROOT, "vit-project_amd", "vit_amd", "lib", "libvit_hip.so")
+    dyn = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-readelf", "-d", "--dyn-syms", so], capture_output=True,
+                         text=True, check=True).stdout.lower()
+    for name in ("hipblaslt", "rocblas", "hipblas"):
+        assert name not in dyn, f"libvit_hip.so references {name}"
+
+
 def test_library_is_gfx950_code_object(tmp_path):
     import shutil
     import subprocess

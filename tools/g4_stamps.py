@@ -68,7 +68,8 @@ def main():
     m0 = (B // 2 + 3 * B // 64) * 197
     cases = [("fwd", "qkv", m0, 3 * D, D), ("fwd", "proj", m0, D, D), ("fwd", "fc2", m0, D, Fh),
              ("dgrad", "qkv", B * 197, 3 * D, D), ("dgrad", "fc1", B * 197, Fh, D), ("dgrad", "proj", B * 197, D, D),
-             ("gelu", "fc2", B * 197, D, Fh)]  # gelu: the fc2 GELU' input gradient with its column sums
+             ("gelu", "fc2", B * 197, D, Fh),  # gelu: the fc2 GELU' input gradient with its column sums
+             ("pair", "fc1", m0, Fh, D)]  # pair: the fc1 GELU pair forward (vit_gemm_g4_gelu bit 1)
     if a.shapes:
         keep = set(a.shapes.split(","))
         cases = [c for c in cases if f"{c[0]}_{c[1]}" in keep]
@@ -78,7 +79,13 @@ def main():
     for kind, nm, M, N, K in cases:
         g = torch.Generator(device=dev).manual_seed(1)
         w = (torch.randn(N, K, device=dev, generator=g) * 0.05).to(bf)
-        if kind == "fwd":
+        if kind == "pair":
+            x = torch.randn(M, K, device=dev, generator=g).to(bf)
+            b = torch.randn(N, device=dev, generator=g)
+            lib.vit_gemm_g4_gelu(3)
+            run = lambda: ops.linear_fwd(x, w, b, epi=L.EPI_BIAS_GELU)  # noqa: E731
+            nk, tiles = K // 64, ((M + 255) // 256) * (N // 256)
+        elif kind == "fwd":
             x = torch.randn(M, K, device=dev, generator=g).to(bf)
             b = torch.randn(N, device=dev, generator=g)
             run = lambda: ops.linear_fwd(x, w, b)  # noqa: E731

@@ -88,6 +88,28 @@ __device__ __forceinline__ void gelu_fast_both(float x, float& g, float& gp) {
   g = x * cdf;
   gp = fmaf(x * 0.39894228040143268f, e, cdf);
 }
+// The same on two elements at once, op for op (so bit for bit: the compiled gelu_fast_both is the sequence
+// below, `__expf(v)` being exp2(v * -log2(e)) here with v = |z|^2): the FMAs and multiplies become
+// v_pk_fma_f32 / v_pk_mul_f32, which do two lanes' worth each; rcp / exp / copysign stay per element.
+// 21 instructions per pair instead of 34 -- the GELU pair epilogues' VALU time.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void gelu_fast_both2(f32x2 x, f32x2& g, f32x2& gp) {
+  const f32x2 z = x * 0.70710678118654752f;
+  const f32x2 az = __builtin_elementwise_abs(z);
+  const f32x2 den = __builtin_elementwise_fma(az, f32x2(0.3275911f), f32x2(1.0f));
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  const f32x2 q = (az * az) * -1.44269504088896341f;
+  const f32x2 e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  f32x2 p = __builtin_elementwise_fma(f32x2(1.061405429f), t, f32x2(-1.453152027f));
+  p = __builtin_elementwise_fma(p, t, f32x2(1.421413741f));
+  p = __builtin_elementwise_fma(p, t, f32x2(-0.284496736f));
+  p = __builtin_elementwise_fma(p, t, f32x2(0.254829592f));
+  const f32x2 y = __builtin_elementwise_fma(-e, t * p, f32x2(1.0f));
+  const f32x2 cs = {copysignf(y.x, z.x), copysignf(y.y, z.y)};
+  const f32x2 cdf = __builtin_elementwise_fma(cs, f32x2(0.5f), f32x2(0.5f));
+  g = x * cdf;
+  gp = __builtin_elementwise_fma(x * 0.39894228040143268f, e, cdf);
+}
 __device__ __forceinline__ void gelu_erf_both(float x, float& g, float& gp) {
   const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752f));
   g = x * cdf;

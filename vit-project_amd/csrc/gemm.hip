@@ -415,13 +415,24 @@ __device__ __forceinline__ void epilogue_pair16(const Epi& e, const f32x4 (&acc)
         *reinterpret_cast<bf16x8*>((bf16*)e.C + (int64_t)i * e.ldc + j) = x;
       } else {
         VecF<8> av, dv;
+        if constexpr (EPI == EPI_BIAS_GELU) {  // two elements per call (packed FP32; same bits)
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          float ga, gd;
-          if constexpr (EPI == EPI_BIAS_GELU) gelu_fast_both((float)x[q], ga, gd);
-          else quick_gelu_both((float)x[q], ga, gd);
-          av.q[q >> 2][q & 3] = ga;
-          dv.q[q >> 2][q & 3] = gd;
+          for (int q = 0; q < 8; q += 2) {
+            f32x2 ga, gd;
+            gelu_fast_both2(f32x2{(float)x[q], (float)x[q + 1]}, ga, gd);
+            av.q[q >> 2][q & 3] = ga.x;
+            av.q[q >> 2][(q & 3) + 1] = ga.y;
+            dv.q[q >> 2][q & 3] = gd.x;
+            dv.q[q >> 2][(q & 3) + 1] = gd.y;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float ga, gd;
+            quick_gelu_both((float)x[q], ga, gd);
+            av.q[q >> 2][q & 3] = ga;
+            dv.q[q >> 2][q & 3] = gd;
+          }
         }
         vstore<bf16, 8>((bf16*)e.C + (int64_t)i * e.ldc + j, dv);
         vstore<bf16, 8>((bf16*)e.aux_out + (int64_t)i * e.ldc + j, av);

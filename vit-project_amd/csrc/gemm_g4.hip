@@ -537,11 +537,13 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
           const bf16x8 x = *reinterpret_cast<const bf16x8*>(smem + r * PITCH + c * 16);
           bf16x8 av, dv;
 #pragma unroll
-          for (int t = 0; t < 8; ++t) {
-            float ga, gd;
-            gelu_fast_both((float)x[t], ga, gd);
-            av[t] = (bf16)ga;
-            dv[t] = (bf16)gd;
+          for (int t = 0; t < 8; t += 2) {
+            f32x2 ga, gd;
+            gelu_fast_both2(f32x2{(float)x[t], (float)x[t + 1]}, ga, gd);
+            av[t] = (bf16)ga.x;
+            av[t + 1] = (bf16)ga.y;
+            dv[t] = (bf16)gd.x;
+            dv[t + 1] = (bf16)gd.y;
           }
           const bool ok = i0 + r < M && col < N;
           store16(__builtin_bit_cast(i32x4, dv), i0 + r, col, ok);
