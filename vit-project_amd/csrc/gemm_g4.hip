@@ -698,7 +698,7 @@ int g4_launch(int q_layout, int ep, const void* P, int64_t ldp, const void* Q, i
   }
   if (ep == 1) {  // GELU' input gradient: C = (P Q^T) * aux, column partials allowed; no bias
     if (!(g_g4[6] & 1) || q_layout != LAY_CR || !e.aux || e.bias || R < 2 * g4::BK || e.ld_aux % 8 || ((uintptr_t)e.aux & 15) ||
-        e.ld_aux >= (1 << 23) ||
+        e.ld_aux >= (1 << 23) || M >= (1 << 24) ||  // aux_off's 24-bit multiplies
         (int64_t)M * e.ld_aux * 2 >= ((int64_t)1 << 31))
       return -1;
     return launch<LAY_CR>(1, P, ldp, Q, ldq, M, N, R, e, s);
