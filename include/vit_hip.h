@@ -62,7 +62,9 @@ int vit_gemm_group(int fwd, int dgrad);
 /* The plain bf16 forward (+ f32 bias) and input-gradient GEMMs run the 4-wave g4 kernel (csrc/gemm_g4.hip,
  * VIT:139 / VIT:142 through timm's qkv / proj / fc1 / fc2).  Tuning / test hook: its tile walk for the forward
  * and the input-gradient class (0 = stride over the tiles with min(tiles, CUs or `wgs`) persistent workgroups,
- * 1 = one workgroup per 256-row band walking the column tiles, -1 = keep), the stride walk's workgroup cap
+ * 1 = one workgroup per 256-row band walking the column tiles, 2 = stride over the tiles with one workgroup per
+ * 256-row band, so the workgroups running together share a band's rows in L2 (the input gradients' default,
+ * round 6: +1.1 / +1.3 % over 1), -1 = keep), the stride walk's workgroup cap
  * (0 = the CU count, -1 = keep) and its tiles per workgroup (grid >= ceil(tiles / tpw); 0 = no limit, -1 = keep). */
 int vit_gemm_g4_config(int fwd_mode, int dgrad_mode, int wgs, int tpw);
 

@@ -586,13 +586,14 @@ def test_g4_plain_gemms_bitwise_match_8wave_kernels(M, N, K):
     _close(y4, (x.double() @ w.double().t() + b.double()).float(), 8e-3, "g4 fwd vs fp64")
 
 
-@pytest.mark.parametrize("fwd_mode,dgrad_mode,wgs,tpw", [(0, 1, 0, 1), (0, 1, 0, 0), (1, 0, 0, 0), (0, 0, 7, 0),
-                                                    (0, 0, 1, 0), (1, 1, 0, 0), (0, 0, 0, 2)])
+@pytest.mark.parametrize("fwd_mode,dgrad_mode,wgs,tpw", [(0, 2, 0, 1), (0, 1, 0, 0), (1, 0, 0, 0), (0, 0, 7, 0),
+                                                    (0, 0, 1, 0), (1, 1, 0, 0), (0, 0, 0, 2), (2, 2, 0, 0)])
 @pytest.mark.parametrize("M,N,K", [(1, 64, 64), (257, 136, 192), (197 * 3, 640, 448), (2000, 1088, 64),
                                    (513, 256, 3072), (300, 8, 128)])
 def test_g4_tile_walks_and_ragged_shapes(fwd_mode, dgrad_mode, wgs, tpw, M, N, K):
     """Every tile walk (stride over G persistent workgroups, G = CUs / 7 / 1 -- one workgroup running every
-    tile in sequence -- or ceil(tiles / tpw) workgroups of at most 1 / 2 tiles, and the row-band walk) on ragged shapes: M = 1 and 257 (a 1-row last tile), output
+    tile in sequence -- or ceil(tiles / tpw) workgroups of at most 1 / 2 tiles, or tiles_i workgroups (walk 2, the
+    input gradients' default), and the row-band walk) on ragged shapes: M = 1 and 257 (a 1-row last tile), output
     widths 8 / 136 / 448 / 1088 (partial 8-column chunks of the last column tile), a single k-step (K = 64)
     and long reductions; the stage stream crosses tile boundaries with 1..48 k-steps per tile.  The forward
     runs on g4 whenever K % 64 == 0 and N % 8 == 0, the input gradient (reduction N) when N % 64 == 0;
@@ -610,7 +611,7 @@ def test_g4_tile_walks_and_ragged_shapes(fwd_mode, dgrad_mode, wgs, tpw, M, N, K
         y4, d4 = _g4_pair(x, w, b, dy)
         assert lib.vit_gemm_g4_count(1) == int(fwd_g4) + int(dgrad_g4)
     finally:
-        lib.vit_gemm_g4_config(0, 1, 0, 1)
+        lib.vit_gemm_g4_config(0, 2, 0, 1)
     y5, _ = _g4_pair(x, w, b, dy, variant=5)
     _, d1 = _g4_pair(x, w, b, dy, variant=1)
     if fwd_g4:

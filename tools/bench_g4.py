@@ -82,16 +82,16 @@ def main():
                 for fm in (1, 0):
                     lib.vit_gemm_g4_config(fm, -1, -1, -1)
                     rec[f"g4_wt_walk{fm}"] = round(flop / timeit(lambda: ops.linear_fwd(dy, wt, None, out=dx), a.reps) / 1e12, 1)
-                lib.vit_gemm_g4_config(0, 1, 0, 1)
-        walks = [(0, 1, 0)]
+                lib.vit_gemm_g4_config(0, 2, 0, 1)
+        walks = [(0, 2, 0)]
         if a.walks:
-            walks = [(0, 1, 0), (1, 1, 0), (0, 0, 0)] if kind == "fwd" else [(0, 1, 0), (0, 0, 0)]
+            walks = [(0, 2, 0), (1, 2, 0)] if kind == "fwd" else [(0, 2, 0), (0, 1, 0), (0, 0, 0)]
         for _ in range(a.rounds):
             for wk in walks:
                 lib.vit_gemm_g4_config(*wk, -1)
-                key = "g4" if wk == (0, 1, 0) else f"g4_walk{wk[0] if kind == 'fwd' else wk[1]}"
+                key = "g4" if wk == (0, 2, 0) else f"g4_walk{wk[0] if kind == 'fwd' else wk[1]}"
                 rec.setdefault(key, []).append(round(flop / timeit(ours, a.reps) / 1e12, 1))
-            lib.vit_gemm_g4_config(0, 1, 0, 1)
+            lib.vit_gemm_g4_config(0, 2, 0, 1)
             for v in old:
                 lib.vit_gemm_variant(v)
                 rec.setdefault(f"V{v}", []).append(round(flop / timeit(ours, a.reps) / 1e12, 1))

@@ -574,7 +574,7 @@ __global__ __launch_bounds__(THREADS, 1) void kernel(const bf16* __restrict__ P,
 }  // namespace g4
 
 namespace {
-// VIT_GEMM_G4 (0 = off), VIT_G4_MODE_{FWD,DGRAD} (0 stride, 1 band), VIT_G4_WGS (stride-walk grid cap),
+// VIT_GEMM_G4 (0 = off), VIT_G4_MODE_{FWD,DGRAD} (0 stride, 1 band, 2 stride on tiles_i workgroups), VIT_G4_WGS (stride-walk grid cap),
 // VIT_G4_TPW (stride walk: at most this many tiles per workgroup, 0 = no limit)
 int g_g4[7] = {-2, -2, -2, -2, -2, -2, -2};
 int g_g4_dbg = 0;  // timing switches of the stamped instance (vit_debug_g4_stamps)
@@ -588,7 +588,7 @@ void g4_env() {
   if (g_g4[0] != -2) return;
   g_g4[0] = g4_env_int("VIT_GEMM_G4", 1);
   g_g4[1] = g4_env_int("VIT_G4_MODE_FWD", 0);
-  g_g4[2] = g4_env_int("VIT_G4_MODE_DGRAD", 1);
+  g_g4[2] = g4_env_int("VIT_G4_MODE_DGRAD", 2);  // 2: +1.1 / +1.3 % over the row bands (two same-box A/Bs)
   g_g4[3] = g4_env_int("VIT_G4_WGS", 0);
   g_g4[4] = g4_env_int("VIT_G4_TPW", 1);  // in the step one tile per workgroup measured best for the
                                           // forward (7267 vs 7061-7091 img/s for 2, 3, 3.8 tiles / CU)
@@ -627,9 +627,12 @@ int launch(int ep, const void* P, int64_t ldp, const void* Q, int64_t ldq, int M
   w.tiles_j = (N + 255) / 256;
   w.group_m = QL == LAY_RC ? e.group_m : 0;
   w.epi = g_g4[5];
-  w.mode = g_g4[QL == LAY_RC ? 1 : 2] == 1 ? 1 : 0;
+  const int wm = g_g4[QL == LAY_RC ? 1 : 2];
+  w.mode = wm == 1 ? 1 : 0;
   if (w.mode == 1) {
     w.G = w.tiles_i;
+  } else if (wm == 2) {  // stride walk on tiles_i workgroups (A/B): band mode's footprint, but the WGs
+    w.G = w.tiles_i;     // running together cover a band's column tiles (its dY rows shared in L2)
   } else {
     const int tiles = w.tiles_i * w.tiles_j, cap = g_g4[3] > 0 ? g_g4[3] : g4_cus();
     w.G = tiles < cap ? tiles : cap;
@@ -710,8 +713,8 @@ int g4_launch(int q_layout, int ep, const void* P, int64_t ldp, const void* Q, i
 
 extern "C" {
 
-// Tuning / test hook: tile walk of the forward and input-gradient classes (0 = stride, 1 = row band, -1 =
-// keep), the stride walk's workgroup cap (0 = the CU count, -1 = keep) and its tiles per workgroup (the
+// Tuning / test hook: tile walk of the forward and input-gradient classes (0 = stride, 1 = row band, 2 = stride
+// over tiles_i persistent workgroups (the input gradients' default), -1 = keep), the stride walk's workgroup cap (0 = the CU count, -1 = keep) and its tiles per workgroup (the
 // grid grows to ceil(tiles / tpw) workgroups; 0 = no limit, -1 = keep).  Returns 0.
 int vit_gemm_g4_config(int fwd_mode, int dgrad_mode, int wgs, int tpw) {
   g4_env();
